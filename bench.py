@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Benchmark: residual+Jacobian evaluations/sec on BAL problem-13682 (MI355X).
+
+One "step" = one residual+Jacobian evaluation of a problem-13682-shaped
+Program (13,682 cameras, 4,456,117 points, 28,987,644 SnavelyReprojectionError
+<2,9,3> residual blocks, HuberLoss(1.0), BlockSparseMatrix with the points
+eliminated first: BASELINE.json configs[3]) through the C ABI's
+device-resident entry point (cse_evaluate_device: residuals, Jacobian values
+and cost written to HBM; inputs already resident when the clock starts).
+
+Multi-GPU (one process per GPU, launched by torch.distributed.run):
+  --scaling weak   (default) every rank evaluates its own problem-13682-sized
+                   shard (a distinct seed) of an N x larger global problem;
+                   the scalar cost is all-reduced over RCCL each step.
+                   value = N * steps / time.
+  --scaling strong the one problem-13682 is partitioned at point-bucket
+                   boundaries (BASELINE.json configs[4]); each rank writes
+                   its contiguous Jacobian strips; cost all-reduced over RCCL.
+                   value = steps / time.
+
+Data is synthetic (no BAL file is available offline; see
+ceres_amd/bal.py for the generator), with the exact BAL header counts.
+Rank 0 prints one JSON line; see DESIGN.md §5 for every field.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
+
+import ceres_amd as ca  # noqa: E402
+from ceres_amd import bal  # noqa: E402
+
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "residual+Jacobian evaluations/sec on BAL problem-13682; achieved HBM GB/s"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="problem-13682-4456117", choices=list(bal.CONFIGS))
+    ap.add_argument("--loss", default="huber", choices=["trivial", "huber", "cauchy"])
+    ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--gradient", action="store_true", help="also produce the gradient J^T r")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-blocks", type=int, default=2_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--seed", type=int, default=0xCE2E5)
+    return ap.parse_args()
+
+
+def make_loss(name):
+    return {"trivial": ca.Loss.trivial(), "huber": ca.Loss.huber(1.0),
+            "cauchy": ca.Loss.cauchy(1.0)}[name]
+
+
+def point_bucket_cuts(pt_idx, num_points, world):
+    """Shard boundaries over residual blocks at point-bucket boundaries
+    (SURVEY.md §8(e)): rank r gets points [pc[r], pc[r+1]) and the blocks
+    [bc[r], bc[r+1]) observing them."""
+    counts = np.bincount(pt_idx, minlength=num_points)
+    csum = np.concatenate([[0], np.cumsum(counts)])
+    O = int(csum[-1])
+    pc = [0]
+    for r in range(1, world):
+        pc.append(int(np.searchsorted(csum, O * r // world)))
+    pc.append(num_points)
+    bc = [int(csum[p]) for p in pc]
+    return pc, bc
+
+
+def build_shard(args, rank, world):
+    counts = bal.CONFIGS[args.config]
+    loss = make_loss(args.loss)
+    if args.scaling == "weak" or world == 1:
+        cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed + rank)
+        prog = bal.program(cams, pts, ci, pi, obs, loss=loss, format=args.format)
+        return prog, {"blocks": int(counts[2]), "strip": None}
+    cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed)
+    pc, bc = point_bucket_cuts(pi, pts.shape[0], world)
+    p0, p1, b0, b1 = pc[rank], pc[rank + 1], bc[rank], bc[rank + 1]
+    prog = bal.program(cams, pts[p0:p1], ci[b0:b1], pi[b0:b1] - p0, obs[b0:b1], loss=loss,
+                       format=args.format)
+    O = int(counts[2])
+    strip = ({"E": [6 * b0, 6 * b1], "F": [6 * O + 18 * b0, 6 * O + 18 * b1]}
+             if args.format == "block_sparse" else {"rows": [24 * b0, 24 * b1]})
+    return prog, {"blocks": b1 - b0, "strip": strip}
+
+
+def cpu_baseline(args, threads):
+    """The oracle (CPU restatement of Ceres' ProgramEvaluator, oracle/) on a
+    bounded, point-bucket-aligned sample of the same workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py as O
+    counts = bal.CONFIGS[args.config]
+    cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed)
+    S = min(args.cpu_sample_blocks, counts[2])
+    # Cut at a point-bucket boundary.
+    last_pt = int(pi[S - 1])
+    S = int(np.searchsorted(pi, last_pt, side="right"))
+    np_ = last_pt + 1
+    prog = bal.program(cams, pts[:np_], ci[:S], pi[:S], obs[:S], loss=make_loss(args.loss),
+                       format=args.format)
+    op = O.OracleProgram.from_program(prog)
+    ev = op.evaluator(threads)
+    r = np.empty(prog.num_residuals)
+    j = np.empty(prog.num_jacobian_values)
+    g = np.empty(prog.num_effective_parameters) if args.gradient else None
+    ev.run(prog.state, None, r, g, j)  # warm-up
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ok, _ = ev.run(prog.state, None, r, g, j)
+        times.append(time.perf_counter() - t0)
+        assert ok
+    ev.close()
+    t = float(np.median(times))
+    blocks_per_s = S / t
+    return {"value": blocks_per_s / counts[2], "unit": "evals/s", "cores": threads,
+            "kind": "port",
+            "sample": f"first {S:,} of {counts[2]:,} residual blocks (point-bucket aligned) of the "
+                      f"same workload, residual+Jacobian{'+gradient' if args.gradient else ''}, "
+                      f"median of 3 evals = {t * 1e3:.1f} ms; value = blocks/s / {counts[2]:,}",
+            "blocks_per_sec": blocks_per_s}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    t_build = time.perf_counter()
+    prog, shard = build_shard(args, rank, world)
+    build_s = time.perf_counter() - t_build
+
+    stream = torch.cuda.current_stream(dev)
+    ev = ca.Evaluator(prog, device=local_rank, profile=True, stream=stream.cuda_stream)
+    info = ev.info()
+    f64 = torch.float64
+    state = torch.from_numpy(prog.state).to(dev)
+    cost = torch.zeros(1, dtype=f64, device=dev)
+    res = torch.empty(prog.num_residuals, dtype=f64, device=dev)
+    jac = torch.empty(prog.num_jacobian_values, dtype=f64, device=dev)
+    grad = torch.empty(prog.num_effective_parameters, dtype=f64, device=dev) if args.gradient else None
+    gptr = grad.data_ptr() if grad is not None else None
+
+    def step():
+        ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), gptr, jac.data_ptr())
+        if world > 1:
+            dist.all_reduce(cost)  # RCCL over xGMI: the global cost
+
+    for _ in range(args.warmup):
+        step()
+    status = ev.wait()
+    if status != 0:
+        raise SystemExit(f"rank {rank}: evaluation failed during warm-up (status {status})")
+    ev.reset_kernel_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    status = ev.wait()
+    last_ms, total_ms, launches = ev.kernel_stats()
+    kernel_ms = total_ms / max(launches, 1)
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=f64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms_max = float(t[0]), float(t[1])
+        ok = torch.tensor([status], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MAX)
+        status = int(ok.item())
+    else:
+        kernel_ms_max = kernel_ms
+    if status != 0:
+        raise SystemExit(f"evaluation failed (status {status})")
+
+    bytes_per_launch = info.bytes_jacobian_eval
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    weak = args.scaling == "weak" or world == 1
+    value = (world if weak else 1) * args.steps / elapsed
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+            cpu = cpu_baseline(args, threads)
+        traffic = None
+        pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}_{args.loss}_{args.format}.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as fh:
+                pmc = json.load(fh)
+            traffic = pmc.get("hbm_bytes_per_launch")
+        C_, P_, O_ = bal.CONFIGS[args.config]
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak" if weak else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (BAL-shaped: exact header counts, seeded generator)",
+            "config": {
+                "workload": f"{args.config} SnavelyReprojectionError<2,9,3> "
+                            f"{args.loss} {args.format} residual+Jacobian"
+                            f"{'+gradient' if args.gradient else ''}, device-resident",
+                "cameras": C_, "points": P_, "observations": O_,
+                "blocks_per_rank": shard["blocks"],
+                "parallelism": ("replica shards per rank" if weak and world > 1 else
+                                "point-bucket block sharding" if world > 1 else "single GPU"),
+                "strip_rank0": shard["strip"],
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": PEAK_HBM_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBPS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "kernel_ms_avg": kernel_ms,
+                "kernel_ms_avg_max_rank": kernel_ms_max,
+                "kernel": "cse::EvaluateGroupKernel<SnavelyKind,...,affine>",
+            },
+            "cpu_baseline": cpu,
+            "speedup_vs_cpu": (value / world / cpu["value"]) if cpu else None,
+            "build_s": build_s,
+            "reference_published": {"value": 0.6455, "unit": "evals/s",
+                                    "what": "V100 Jacobian&residual eval incl. H2D/D2H, no loss, "
+                                            "README.md:189 (not the same metric)"},
+        }
+        print(json.dumps(out), flush=True)
+    ev.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

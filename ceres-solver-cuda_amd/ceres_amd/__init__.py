@@ -1,0 +1,18 @@
+"""ceres_amd: Python host side of the MI355X (gfx950) residual/Jacobian
+evaluator for Ceres' ProblemCUDA / AutoDiffCostFunction residual blocks.
+
+The compute path is libcse.so (HIP kernels behind the C ABI in
+include/cse.h); this package builds Programs and calls it.  There is no
+CPU fallback anywhere in the package.
+"""
+from . import _cse, bal
+from ._cse import (LOSS_CAUCHY, LOSS_HUBER, LOSS_TRIVIAL, POINT_DISPLACEMENT_3_3,
+                   SNAVELY_2_9_3, SNAVELY_NO_DISTORTION_2_7_3, SNAVELY_QUATERNION_2_10_3,
+                   FUNCTOR_SHAPES)
+from .problem import (BLOCK_SPARSE, COMPRESSED_ROW, Evaluator, Loss, Program, ProblemCUDA,
+                      ResidualGroup)
+
+__all__ = ["bal", "Evaluator", "Loss", "Program", "ProblemCUDA", "ResidualGroup",
+           "BLOCK_SPARSE", "COMPRESSED_ROW", "SNAVELY_2_9_3", "SNAVELY_NO_DISTORTION_2_7_3",
+           "SNAVELY_QUATERNION_2_10_3", "POINT_DISPLACEMENT_3_3", "LOSS_TRIVIAL", "LOSS_HUBER",
+           "LOSS_CAUCHY", "FUNCTOR_SHAPES"]

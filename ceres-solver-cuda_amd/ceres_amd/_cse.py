@@ -1,0 +1,153 @@
+"""ctypes binding of include/cse.h (the C ABI of libcse.so).
+
+The library is loaded from ceres-solver-cuda_amd/lib/libcse.so (built by
+`make` in ceres-solver-cuda_amd/ or __graft_entry__.build()).  There is no
+fallback: if the library is missing, loading raises.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libcse.so"))
+
+CSE_ABI_VERSION = 1
+CSE_OK = 0
+CSE_EVALUATION_FAILED = 1
+CSE_ERR_INVALID = -1
+CSE_ERR_HIP = -2
+CSE_ERR_OOM = -3
+CSE_ERR_UNSUPPORTED = -4
+
+# cse_functor_kind
+SNAVELY_2_9_3 = 0
+SNAVELY_NO_DISTORTION_2_7_3 = 1
+SNAVELY_QUATERNION_2_10_3 = 2
+POINT_DISPLACEMENT_3_3 = 3
+
+# (num_residuals, parameter block sizes, functor data size)
+FUNCTOR_SHAPES = {
+    SNAVELY_2_9_3: (2, (9, 3), 2),
+    SNAVELY_NO_DISTORTION_2_7_3: (2, (7, 3), 2),
+    SNAVELY_QUATERNION_2_10_3: (2, (10, 3), 2),
+    POINT_DISPLACEMENT_3_3: (3, (3,), 3),
+}
+
+# cse_loss_kind
+LOSS_TRIVIAL = 0
+LOSS_HUBER = 1
+LOSS_CAUCHY = 2
+
+
+class cse_loss(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("scaled", C.c_int32), ("a", C.c_double),
+                ("scale", C.c_double)]
+
+
+class cse_parameter_block(C.Structure):
+    _fields_ = [("size", C.c_int32), ("tangent_size", C.c_int32),
+                ("is_constant", C.c_int32), ("reserved", C.c_int32),
+                ("state_offset", C.c_int64), ("delta_offset", C.c_int64),
+                ("plus_jacobian_offset", C.c_int64)]
+
+
+class cse_residual_group(C.Structure):
+    _fields_ = [("functor_kind", C.c_int32), ("reserved", C.c_int32),
+                ("loss", cse_loss), ("num_blocks", C.c_int64),
+                ("residual_block_index", C.POINTER(C.c_int64)),
+                ("first_residual_block", C.c_int64),
+                ("parameter_block_ids", C.POINTER(C.c_int32)),
+                ("functor_data", C.POINTER(C.c_double))]
+
+
+class cse_problem_desc(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("num_groups", C.c_int32),
+                ("groups", C.POINTER(cse_residual_group)),
+                ("num_parameter_blocks", C.c_int64),
+                ("parameter_blocks", C.POINTER(cse_parameter_block)),
+                ("num_parameters", C.c_int64), ("num_effective_parameters", C.c_int64),
+                ("num_constant_parameters", C.c_int64),
+                ("constant_state", C.POINTER(C.c_double)),
+                ("num_plus_jacobian_values", C.c_int64),
+                ("plus_jacobians", C.POINTER(C.c_double)),
+                ("num_residual_blocks", C.c_int64), ("num_residuals", C.c_int64),
+                ("residual_layout", C.POINTER(C.c_int64)),
+                ("jacobian_per_residual_layout", C.POINTER(C.c_int64)),
+                ("jacobian_per_residual_offsets", C.POINTER(C.c_int64)),
+                ("num_jacobian_per_residual_offsets", C.c_int64),
+                ("num_jacobian_values", C.c_int64)]
+
+
+class cse_options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("check_finite", C.c_int32),
+                ("apply_loss_function", C.c_int32), ("force_general_layout", C.c_int32),
+                ("profile", C.c_int32), ("reserved", C.c_int32), ("stream", C.c_void_p)]
+
+
+class cse_info(C.Structure):
+    _fields_ = [("num_residual_blocks", C.c_int64), ("num_residuals", C.c_int64),
+                ("num_parameters", C.c_int64), ("num_effective_parameters", C.c_int64),
+                ("num_jacobian_values", C.c_int64), ("num_groups", C.c_int32),
+                ("num_affine_groups", C.c_int32), ("device", C.c_int32),
+                ("reserved", C.c_int32), ("bytes_jacobian_eval", C.c_int64),
+                ("bytes_residual_eval", C.c_int64)]
+
+
+P_i32 = C.POINTER(C.c_int32)
+P_i64 = C.POINTER(C.c_int64)
+P_f64 = C.POINTER(C.c_double)
+P_pb = C.POINTER(cse_parameter_block)
+
+# Every exported symbol of include/cse.h with its signature.
+SIGNATURES = {
+    "cse_default_options": (None, [C.POINTER(cse_options)]),
+    "cse_create": (C.c_int, [C.POINTER(cse_problem_desc), C.POINTER(cse_options),
+                             C.POINTER(C.c_void_p)]),
+    "cse_evaluate": (C.c_int, [C.c_void_p, P_f64, P_f64, P_f64, P_f64, P_f64]),
+    "cse_evaluate_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]),
+    "cse_wait": (C.c_int, [C.c_void_p]),
+    "cse_set_plus_jacobians": (C.c_int, [C.c_void_p, P_f64]),
+    "cse_destroy": (None, [C.c_void_p]),
+    "cse_last_error": (C.c_char_p, []),
+    "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),
+    "cse_kernel_stats": (C.c_int, [C.c_void_p, P_f64, P_f64, P_i64]),
+    "cse_reset_kernel_stats": (C.c_int, [C.c_void_p]),
+    "cse_block_sparse_layout": (C.c_int, [C.c_int64, P_pb, C.c_int64, P_i64, P_i32, P_i32,
+                                          C.c_int64, P_i64, P_i64, P_i64, P_i64]),
+    "cse_compressed_row_layout": (C.c_int, [C.c_int64, P_pb, C.c_int64, P_i64, P_i32, P_i32,
+                                            P_i64, P_i64, P_i64, P_i64, P_i64, P_i64]),
+    "cse_layout_offsets_count": (C.c_int64, [C.c_int64, P_pb, C.c_int64, P_i64, P_i32, P_i32]),
+    "cse_abi_version": (C.c_int, []),
+    "cse_build_info": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libcse.so once.  Raises if the HIP library has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libcse.so not found at {LIB_PATH}: build it with `make -C "
+                f"ceres-solver-cuda_amd` (there is no CPU fallback)")
+        handle = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        if handle.cse_abi_version() != CSE_ABI_VERSION:
+            raise RuntimeError("libcse.so ABI version mismatch")
+        _lib = handle
+    return _lib
+
+
+def last_error():
+    return lib().cse_last_error().decode()
+
+
+def check(rc, what):
+    if rc < 0:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error()}")
+    return rc

@@ -1,0 +1,163 @@
+"""BAL (Bundle Adjustment in the Large) problems for the evaluator.
+
+* synthetic(C, P, O, seed): a BAL-shaped problem with exactly the header
+  counts of a real BAL file; no BAL file is available
+  offline.  Point-major observations, each point seen by floor/ceil(O/P)
+  distinct cameras drawn uniformly without replacement; cameras
+  aa ~ N(0, 0.05^2) (camera 0 exactly zero: the Taylor branch of
+  AngleAxisRotatePoint), t = (N(0,1), N(0,1), -10 + N(0,1)),
+  f ~ U[400, 1200], l1 ~ N(0, 0.05^2), l2 ~ N(0, 0.01^2); points
+  ~ U[-3, 3]^3; obs = projection + N(0, 1) px, 5% outliers U(-50, 50) px.
+* read(path): the BAL text format (examples/bal_problem.cc:72-132).
+* program(...): the Ceres Program for bundle_adjuster's Schur setup
+  (examples/bundle_adjuster.cu.cc:307-353 BuildProblem + the points-first
+  elimination ordering): points are the E blocks (parameter blocks 0..P-1),
+  cameras follow, residual blocks are grouped by point
+  (reorder_program.cc:254-336).
+"""
+import numpy as np
+
+from . import _cse
+from .problem import BLOCK_SPARSE, Loss, Program, ResidualGroup
+
+# (cameras, points, observations) of the BAL files named in BASELINE.json.
+CONFIGS = {
+    "problem-16-22106": (16, 22106, 83718),
+    "problem-1778-993923": (1778, 993923, 5001946),
+    "problem-13682-4456117": (13682, 4456117, 28987644),
+}
+
+
+def project(cameras, points, cam_idx, pt_idx):
+    """Snavely projection in numpy (generator only: observations are the
+    model's prediction plus noise)."""
+    cam = cameras[cam_idx]
+    X = points[pt_idx]
+    aa = cam[:, 0:3]
+    theta = np.sqrt((aa * aa).sum(1))
+    safe = np.where(theta > 0, theta, 1.0)
+    w = aa / safe[:, None]
+    ct, st = np.cos(theta), np.sin(theta)
+    wx = np.cross(w, X)
+    wd = (w * X).sum(1)
+    rot = X * ct[:, None] + wx * st[:, None] + w * (wd * (1 - ct))[:, None]
+    rot0 = X + np.cross(aa, X)
+    p = np.where((theta > 0)[:, None], rot, rot0) + cam[:, 3:6]
+    xp, yp = -p[:, 0] / p[:, 2], -p[:, 1] / p[:, 2]
+    r2 = xp * xp + yp * yp
+    d = 1.0 + r2 * (cam[:, 7] + cam[:, 8] * r2)
+    return np.stack([cam[:, 6] * d * xp, cam[:, 6] * d * yp], 1)
+
+
+def synthetic(num_cameras, num_points, num_observations, seed=0xCE2E5, outlier_fraction=0.05):
+    """Returns (cameras[C,9], points[P,3], cam_idx[O], pt_idx[O], obs[O,2]) in
+    point-major order."""
+    C, P, O = int(num_cameras), int(num_points), int(num_observations)
+    if O < P:
+        raise ValueError("need at least one observation per point")
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cameras = np.empty((C, 9))
+    cameras[:, 0:3] = rng.normal(0.0, 0.05, (C, 3))
+    cameras[0, 0:3] = 0.0
+    cameras[:, 3:5] = rng.normal(0.0, 1.0, (C, 2))
+    cameras[:, 5] = -10.0 + rng.normal(0.0, 1.0, C)
+    cameras[:, 6] = rng.uniform(400.0, 1200.0, C)
+    cameras[:, 7] = rng.normal(0.0, 0.05, C)
+    cameras[:, 8] = rng.normal(0.0, 0.01, C)
+    points = rng.uniform(-3.0, 3.0, (P, 3))
+
+    base, extra = divmod(O, P)
+    if base + (1 if extra else 0) > C:
+        raise ValueError("more observations per point than cameras")
+    counts = np.full(P, base, np.int64)
+    counts[:extra] += 1
+    cam_idx = np.empty(O, np.int32)
+    pt_idx = np.repeat(np.arange(P, dtype=np.int32), counts)
+    starts = np.zeros(P + 1, np.int64)
+    np.cumsum(counts, out=starts[1:])
+    for k, sel in ((base + 1, slice(0, extra)), (base, slice(extra, P))):
+        npts = len(range(*sel.indices(P)))
+        if npts == 0 or k == 0:
+            continue
+        m = _distinct_rows(rng, npts, k, C)
+        first = starts[sel.start]
+        cam_idx[first:first + npts * k] = m.ravel()
+    obs = project(cameras, points, cam_idx, pt_idx)
+    obs += rng.normal(0.0, 1.0, obs.shape)
+    out = rng.random(O) < outlier_fraction
+    obs[out] += rng.uniform(-50.0, 50.0, (int(out.sum()), 2))
+    return cameras, points, cam_idx, pt_idx, obs
+
+
+def _distinct_rows(rng, n, k, C):
+    """n rows of k distinct integers in [0, C)."""
+    m = rng.integers(0, C, (n, k), dtype=np.int32)
+    while True:
+        s = np.sort(m, axis=1)
+        bad = (s[:, 1:] == s[:, :-1]).any(axis=1)
+        nb = int(bad.sum())
+        if nb == 0:
+            return m
+        m[bad] = rng.integers(0, C, (nb, k), dtype=np.int32)
+
+
+def read(path):
+    """BAL text file -> (cameras, points, cam_idx, pt_idx, obs) in file order."""
+    with open(path) as fh:
+        C, P, O = (int(x) for x in fh.readline().split())
+        obs_rows = np.loadtxt(fh, max_rows=O)
+        params = np.loadtxt(fh).ravel()
+    cam_idx = obs_rows[:, 0].astype(np.int32)
+    pt_idx = obs_rows[:, 1].astype(np.int32)
+    obs = obs_rows[:, 2:4].copy()
+    cameras = params[: 9 * C].reshape(C, 9)
+    points = params[9 * C: 9 * C + 3 * P].reshape(P, 3)
+    return cameras, points, cam_idx, pt_idx, obs
+
+
+def schur_residual_order(pt_idx, num_points):
+    """LexicographicallyOrderResidualBlocks (reorder_program.cc:254-336):
+    bucket residual blocks by their E block (point), each bucket filled
+    from the back.  Returns the permutation new_position -> old index."""
+    pt_idx = np.asarray(pt_idx, np.int64)
+    ends = np.cumsum(np.bincount(pt_idx, minlength=num_points))
+    sort = np.argsort(pt_idx, kind="stable")
+    sp = pt_idx[sort]
+    # rank of each block among its point's blocks, in the old order
+    rank = np.empty(len(pt_idx), np.int64)
+    rank[sort] = np.arange(len(sp)) - np.searchsorted(sp, sp, side="left")
+    new_pos = ends[pt_idx] - 1 - rank
+    perm = np.empty(len(pt_idx), np.int64)
+    perm[new_pos] = np.arange(len(pt_idx))
+    return perm
+
+
+def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=_cse.SNAVELY_2_9_3,
+            format=BLOCK_SPARSE, compile=True):
+    """The Schur-ordered Program of a BAL problem (observations must
+    already be point-major, as synthetic() returns and
+    schur_residual_order() produces)."""
+    C, P = cameras.shape[0], points.shape[0]
+    cam_size = cameras.shape[1]
+    npb = P + C
+    pb_size = np.empty(npb, np.int32)
+    pb_size[:P] = 3
+    pb_size[P:] = cam_size
+    ids = np.empty((len(cam_idx), 2), np.int32)
+    ids[:, 0] = P + np.asarray(cam_idx, np.int32)
+    ids[:, 1] = pt_idx
+    group = ResidualGroup(kind, loss or Loss.trivial(), ids, np.ascontiguousarray(obs, np.float64),
+                          None, 0)
+    state = np.concatenate([points.ravel(), cameras.ravel()])
+    prog = Program(pb_size, pb_size.copy(), np.zeros(npb, np.int32), np.full(npb, -1, np.int64),
+                   np.zeros(0), [group], len(cam_idx), state, np.zeros(0))
+    if compile:
+        prog.compile(format, num_eliminate_blocks=P)
+    return prog
+
+
+def synthetic_program(name_or_counts, loss=None, format=BLOCK_SPARSE, seed=0xCE2E5,
+                      compile=True):
+    counts = CONFIGS[name_or_counts] if isinstance(name_or_counts, str) else name_or_counts
+    cams, pts, ci, pi, obs = synthetic(*counts, seed=seed)
+    return program(cams, pts, ci, pi, obs, loss=loss, format=format, compile=compile)

@@ -1,0 +1,396 @@
+"""Host-side Program model and evaluator for Python callers.
+
+Mirrors the reference's ProblemCUDA surface (include/ceres/problem_cuda.h:85-486)
+and the part of Ceres' Program the evaluator consumes:
+
+  * ProblemCUDA.add_parameter_block / set_parameter_block_constant /
+    set_plus_jacobian  (Problem::AddParameterBlock, SetParameterBlockConstant,
+    SetManifold -> the manifold's PlusJacobian);
+  * ProblemCUDA.add_residual_blocks(kind, loss, ids, data): a vectorised
+    ProblemCUDA::AddResidualBlock<Functor, kR, Ns...>(cost, loss, x0, xs...)
+    for many blocks of one (functor, loss) type at once — one
+    "registered CUDA evaluator" (problem_cuda.h:462-468);
+  * Program.compile(format, num_eliminate_blocks): parameter offsets
+    (Program::SetParameterOffsetsAndIndex, program.cc:151-177) and the
+    Jacobian layout of BlockJacobianWriter / CompressedRowJacobianWriter,
+    built by the library's own C++ layout builders;
+  * Evaluator: the ProgramEvaluatorCUDA seam (Evaluate(state, cost,
+    residuals, gradient, jacobian_values)) over libcse.so.
+
+Arrays, not per-block objects: a BAL problem-13682 has 29M residual blocks.
+"""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _cse
+from ._cse import FUNCTOR_SHAPES
+
+BLOCK_SPARSE = "block_sparse"
+COMPRESSED_ROW = "compressed_row"
+
+
+def _ptr(a, ctype):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+@dataclass
+class Loss:
+    """LossFunctionCUDA (include/ceres/loss_function_cuda.h:62-150)."""
+    kind: int = _cse.LOSS_TRIVIAL
+    a: float = 1.0
+    scaled: bool = False
+    scale: float = 1.0
+
+    @staticmethod
+    def trivial():
+        return Loss(_cse.LOSS_TRIVIAL)
+
+    @staticmethod
+    def huber(a):
+        return Loss(_cse.LOSS_HUBER, float(a))
+
+    @staticmethod
+    def cauchy(a):
+        return Loss(_cse.LOSS_CAUCHY, float(a))
+
+    def scaled_by(self, s):
+        return Loss(self.kind, self.a, True, float(s))
+
+
+@dataclass
+class ResidualGroup:
+    kind: int
+    loss: Loss
+    ids: np.ndarray            # (n, num blocks of kind) int32
+    data: np.ndarray           # (n, data size) float64
+    index: Optional[np.ndarray] = None  # (n,) int64 program order; None = contiguous
+    first: int = 0
+
+    @property
+    def n(self):
+        return int(self.ids.shape[0])
+
+
+@dataclass
+class Program:
+    """A reduced Program: parameter blocks and residual groups in program order."""
+    pb_size: np.ndarray
+    pb_tangent: np.ndarray
+    pb_constant: np.ndarray
+    pb_plus_jacobian: np.ndarray
+    plus_jacobians: np.ndarray
+    groups: List[ResidualGroup]
+    num_residual_blocks: int
+    state: np.ndarray           # active parameter blocks, program order
+    constant_state: np.ndarray  # constant parameter blocks
+    # Set by compile().
+    format: str = BLOCK_SPARSE
+    num_eliminate_blocks: int = 0
+    state_offset: np.ndarray = None
+    delta_offset: np.ndarray = None
+    residual_layout: np.ndarray = None
+    jacobian_per_residual_layout: np.ndarray = None
+    jacobian_per_residual_offsets: np.ndarray = None
+    num_jacobian_values: int = 0
+    crs_rows: np.ndarray = None
+    crs_cols: np.ndarray = None
+    _keep: list = field(default_factory=list)
+
+    @property
+    def num_parameter_blocks(self):
+        return int(self.pb_size.shape[0])
+
+    @property
+    def num_parameters(self):
+        return int(self.pb_size[self.pb_constant == 0].sum())
+
+    @property
+    def num_effective_parameters(self):
+        return int(self.pb_tangent[self.pb_constant == 0].sum())
+
+    @property
+    def num_constant_parameters(self):
+        return int(self.pb_size[self.pb_constant != 0].sum())
+
+    def residuals_per_block(self):
+        nres = np.zeros(self.num_residual_blocks, np.int32)
+        for g in self.groups:
+            idx = g.index if g.index is not None else np.arange(g.first, g.first + g.n)
+            nres[idx] = FUNCTOR_SHAPES[g.kind][0]
+        return nres
+
+    @property
+    def num_residuals(self):
+        return int(sum(FUNCTOR_SHAPES[g.kind][0] * g.n for g in self.groups))
+
+    def block_params_csr(self):
+        """(param_begin[nrb+1], param_ids) in program order."""
+        nrb = self.num_residual_blocks
+        nb = np.zeros(nrb, np.int64)
+        for g in self.groups:
+            idx = g.index if g.index is not None else np.arange(g.first, g.first + g.n)
+            nb[idx] = g.ids.shape[1]
+        begin = np.zeros(nrb + 1, np.int64)
+        np.cumsum(nb, out=begin[1:])
+        ids = np.empty(int(begin[-1]), np.int32)
+        for g in self.groups:
+            idx = g.index if g.index is not None else np.arange(g.first, g.first + g.n)
+            k = g.ids.shape[1]
+            pos = begin[idx][:, None] + np.arange(k)[None, :]
+            ids[pos.ravel()] = g.ids.ravel()
+        return begin, ids
+
+    def parameter_blocks_struct(self):
+        npb = self.num_parameter_blocks
+        arr = (_cse.cse_parameter_block * max(npb, 1))()
+        rec = np.frombuffer(arr, dtype=np.dtype([("size", "<i4"), ("tangent_size", "<i4"),
+                                                  ("is_constant", "<i4"), ("reserved", "<i4"),
+                                                  ("state_offset", "<i8"),
+                                                  ("delta_offset", "<i8"),
+                                                  ("plus_jacobian_offset", "<i8")]),
+                            count=max(npb, 1))
+        if npb:
+            rec["size"] = self.pb_size
+            rec["tangent_size"] = self.pb_tangent
+            rec["is_constant"] = self.pb_constant
+            rec["reserved"] = 0
+            rec["state_offset"] = self.state_offset
+            rec["delta_offset"] = self.delta_offset
+            rec["plus_jacobian_offset"] = self.pb_plus_jacobian
+        return arr
+
+    def compile(self, format=BLOCK_SPARSE, num_eliminate_blocks=0):
+        """Offsets (program.cc:151-177) and the Jacobian layout tables."""
+        self.format = format
+        self.num_eliminate_blocks = int(num_eliminate_blocks)
+        const = self.pb_constant != 0
+        so = np.zeros(self.num_parameter_blocks, np.int64)
+        do = np.full(self.num_parameter_blocks, -1, np.int64)
+        act_sizes = np.where(const, 0, self.pb_size).astype(np.int64)
+        act_tan = np.where(const, 0, self.pb_tangent).astype(np.int64)
+        con_sizes = np.where(const, self.pb_size, 0).astype(np.int64)
+        so_act = np.cumsum(act_sizes) - act_sizes
+        so_con = np.cumsum(con_sizes) - con_sizes
+        so[:] = np.where(const, so_con, so_act)
+        do[:] = np.where(const, 0, np.cumsum(act_tan) - act_tan)
+        self.state_offset, self.delta_offset = so, do
+        pbs = self.parameter_blocks_struct()
+        begin, ids = self.block_params_csr()
+        nres = self.residuals_per_block()
+        L = _cse.lib()
+        nrb = self.num_residual_blocks
+        count = L.cse_layout_offsets_count(self.num_parameter_blocks, pbs, nrb, _ptr(begin, C.c_int64),
+                                           _ptr(ids, C.c_int32), _ptr(nres, C.c_int32))
+        self.residual_layout = np.empty(nrb, np.int64)
+        self.jacobian_per_residual_layout = np.empty(nrb, np.int64)
+        self.jacobian_per_residual_offsets = np.empty(max(count, 1), np.int64)
+        nvals = C.c_int64(0)
+        if format == BLOCK_SPARSE:
+            rc = L.cse_block_sparse_layout(
+                self.num_parameter_blocks, pbs, nrb, _ptr(begin, C.c_int64), _ptr(ids, C.c_int32),
+                _ptr(nres, C.c_int32), self.num_eliminate_blocks,
+                _ptr(self.residual_layout, C.c_int64),
+                _ptr(self.jacobian_per_residual_layout, C.c_int64),
+                _ptr(self.jacobian_per_residual_offsets, C.c_int64), C.byref(nvals))
+        elif format == COMPRESSED_ROW:
+            self.crs_rows = np.empty(self.num_residuals + 1, np.int64)
+            rc = L.cse_compressed_row_layout(
+                self.num_parameter_blocks, pbs, nrb, _ptr(begin, C.c_int64), _ptr(ids, C.c_int32),
+                _ptr(nres, C.c_int32), _ptr(self.residual_layout, C.c_int64),
+                _ptr(self.jacobian_per_residual_layout, C.c_int64),
+                _ptr(self.jacobian_per_residual_offsets, C.c_int64), C.byref(nvals),
+                _ptr(self.crs_rows, C.c_int64), None)
+        else:
+            raise ValueError(format)
+        _cse.check(rc, "layout")
+        self.num_jacobian_offsets = int(count)
+        self.num_jacobian_values = int(nvals.value)
+        return self
+
+    def descriptor(self):
+        """cse_problem_desc over this program (arrays kept alive on self)."""
+        assert self.residual_layout is not None, "compile() first"
+        keep = []
+        groups = (_cse.cse_residual_group * max(len(self.groups), 1))()
+        for k, g in enumerate(self.groups):
+            ids = np.ascontiguousarray(g.ids, np.int32)
+            data = np.ascontiguousarray(g.data, np.float64)
+            idx = None if g.index is None else np.ascontiguousarray(g.index, np.int64)
+            keep += [ids, data, idx]
+            groups[k].functor_kind = g.kind
+            groups[k].loss = _cse.cse_loss(g.loss.kind, int(g.loss.scaled), g.loss.a, g.loss.scale)
+            groups[k].num_blocks = g.n
+            groups[k].residual_block_index = _ptr(idx, C.c_int64)
+            groups[k].first_residual_block = g.first
+            groups[k].parameter_block_ids = _ptr(ids, C.c_int32)
+            groups[k].functor_data = _ptr(data, C.c_double)
+        pbs = self.parameter_blocks_struct()
+        cstate = np.ascontiguousarray(self.constant_state, np.float64)
+        pj = np.ascontiguousarray(self.plus_jacobians, np.float64)
+        keep += [groups, pbs, cstate, pj]
+        d = _cse.cse_problem_desc()
+        d.abi_version = _cse.CSE_ABI_VERSION
+        d.num_groups = len(self.groups)
+        d.groups = groups
+        d.num_parameter_blocks = self.num_parameter_blocks
+        d.parameter_blocks = pbs
+        d.num_parameters = self.num_parameters
+        d.num_effective_parameters = self.num_effective_parameters
+        d.num_constant_parameters = self.num_constant_parameters
+        d.constant_state = _ptr(cstate, C.c_double)
+        d.num_plus_jacobian_values = int(pj.size)
+        d.plus_jacobians = _ptr(pj, C.c_double)
+        d.num_residual_blocks = self.num_residual_blocks
+        d.num_residuals = self.num_residuals
+        d.residual_layout = _ptr(self.residual_layout, C.c_int64)
+        d.jacobian_per_residual_layout = _ptr(self.jacobian_per_residual_layout, C.c_int64)
+        d.jacobian_per_residual_offsets = _ptr(self.jacobian_per_residual_offsets, C.c_int64)
+        d.num_jacobian_per_residual_offsets = self.num_jacobian_offsets
+        d.num_jacobian_values = self.num_jacobian_values
+        self._keep = keep
+        return d
+
+
+class ProblemCUDA:
+    """Incremental builder with the reference's ProblemCUDA vocabulary."""
+
+    def __init__(self):
+        self._sizes, self._tangent, self._const, self._pj_off = [], [], [], []
+        self._values = []
+        self._pj = []
+        self._pj_count = 0
+        self._groups = []
+        self._nrb = 0
+
+    def add_parameter_block(self, values):
+        values = np.asarray(values, np.float64)
+        self._sizes.append(values.size)
+        self._tangent.append(values.size)
+        self._const.append(0)
+        self._pj_off.append(-1)
+        self._values.append(values.copy())
+        return len(self._sizes) - 1
+
+    def set_parameter_block_constant(self, b):
+        self._const[b] = 1
+
+    def set_plus_jacobian(self, b, plus_jacobian):
+        """Manifold for block b given by its PlusJacobian (size x tangent)."""
+        pj = np.asarray(plus_jacobian, np.float64)
+        assert pj.shape[0] == self._sizes[b]
+        self._tangent[b] = pj.shape[1]
+        self._pj_off[b] = self._pj_count
+        self._pj.append(pj.ravel())
+        self._pj_count += pj.size
+
+    def add_residual_blocks(self, kind, loss, ids, data):
+        ids = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1, len(FUNCTOR_SHAPES[kind][1])))
+        data = np.ascontiguousarray(np.asarray(data, np.float64).reshape(ids.shape[0], -1))
+        n = ids.shape[0]
+        self._groups.append(ResidualGroup(kind, loss or Loss.trivial(), ids, data, None, self._nrb))
+        self._nrb += n
+        return range(self._nrb - n, self._nrb)
+
+    def add_residual_block(self, kind, loss, data, *blocks):
+        return self.add_residual_blocks(kind, loss, [blocks], [data])[0]
+
+    def program(self, group_by_type=True):
+        """Program order = insertion order.  Blocks sharing (kind, loss) are
+        merged into one group, like the per-type evaluator registry."""
+        groups = self._groups
+        if group_by_type:
+            merged = {}
+            for g in groups:
+                key = (g.kind, g.loss.kind, g.loss.a, g.loss.scaled, g.loss.scale)
+                idx = np.arange(g.first, g.first + g.n, dtype=np.int64)
+                if key in merged:
+                    m = merged[key]
+                    m.ids = np.concatenate([m.ids, g.ids])
+                    m.data = np.concatenate([m.data, g.data])
+                    m.index = np.concatenate([m.index, idx])
+                else:
+                    merged[key] = ResidualGroup(g.kind, g.loss, g.ids, g.data, idx, 0)
+            groups = list(merged.values())
+            for g in groups:
+                if np.array_equal(g.index, np.arange(g.index[0], g.index[0] + g.n)):
+                    g.first, g.index = int(g.index[0]), None
+        const = np.array(self._const, np.int32)
+        values = self._values
+        state = np.concatenate([v for v, c in zip(values, const) if not c] or [np.zeros(0)])
+        cstate = np.concatenate([v for v, c in zip(values, const) if c] or [np.zeros(0)])
+        pj = np.concatenate(self._pj) if self._pj else np.zeros(0)
+        return Program(np.array(self._sizes, np.int32), np.array(self._tangent, np.int32), const,
+                       np.array(self._pj_off, np.int64), pj, groups, self._nrb, state, cstate)
+
+
+class Evaluator:
+    """ProgramEvaluatorCUDA seam over libcse.so (program_evaluator_cuda.h:65-183)."""
+
+    def __init__(self, program, device=-1, check_finite=True, apply_loss_function=True,
+                 force_general_layout=False, profile=False, stream=None):
+        self.program = program
+        self.desc = program.descriptor()
+        opts = _cse.cse_options()
+        L = _cse.lib()
+        L.cse_default_options(C.byref(opts))
+        opts.device = device
+        opts.check_finite = int(check_finite)
+        opts.apply_loss_function = int(apply_loss_function)
+        opts.force_general_layout = int(force_general_layout)
+        opts.profile = int(profile)
+        opts.stream = stream
+        h = C.c_void_p()
+        _cse.check(L.cse_create(C.byref(self.desc), C.byref(opts), C.byref(h)), "cse_create")
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _cse.lib().cse_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        inf = _cse.cse_info()
+        _cse.check(_cse.lib().cse_get_info(self.handle, C.byref(inf)), "cse_get_info")
+        return inf
+
+    def evaluate(self, state=None, residuals=True, gradient=True, jacobian=True):
+        """Host-pointer Evaluate.  Returns (ok, cost, residuals, gradient, jacobian)."""
+        p = self.program
+        state = np.ascontiguousarray(p.state if state is None else state, np.float64)
+        cost = C.c_double(-1.0)
+        r = np.empty(p.num_residuals) if residuals else None
+        g = np.empty(p.num_effective_parameters) if gradient else None
+        j = np.empty(p.num_jacobian_values) if jacobian else None
+        rc = _cse.lib().cse_evaluate(self.handle, _ptr(state, C.c_double), C.byref(cost),
+                                     _ptr(r, C.c_double), _ptr(g, C.c_double), _ptr(j, C.c_double))
+        _cse.check(rc, "cse_evaluate")
+        return rc == _cse.CSE_OK, cost.value, r, g, j
+
+    def evaluate_device(self, d_state, d_cost, d_residuals=None, d_gradient=None, d_jacobian=None):
+        """Device-pointer Evaluate (integers = device addresses).  Async."""
+        rc = _cse.lib().cse_evaluate_device(self.handle, d_state, d_cost, d_residuals, d_gradient,
+                                            d_jacobian)
+        return _cse.check(rc, "cse_evaluate_device")
+
+    def wait(self):
+        return _cse.check(_cse.lib().cse_wait(self.handle), "cse_wait")
+
+    def kernel_stats(self):
+        last, total, n = C.c_double(), C.c_double(), C.c_int64()
+        _cse.check(_cse.lib().cse_kernel_stats(self.handle, C.byref(last), C.byref(total),
+                                               C.byref(n)), "cse_kernel_stats")
+        return last.value, total.value, n.value
+
+    def reset_kernel_stats(self):
+        _cse.check(_cse.lib().cse_reset_kernel_stats(self.handle), "cse_reset_kernel_stats")

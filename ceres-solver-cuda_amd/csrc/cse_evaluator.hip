@@ -1,0 +1,664 @@
+// cse_evaluator.hip -- the C ABI (include/cse.h) over the gfx950 kernels.
+//
+// Host side of the evaluator: validates and uploads the Program once
+// (RegisteredCUDAEvaluators::Init, internal/ceres/registered_cuda_evaluators.cc:226-280),
+// picks a layout policy per residual group, and runs one fused kernel per
+// group plus one finalize kernel per evaluation
+// (RegisteredCUDAEvaluators::Evaluate, :46-103).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/cse.h"
+#include "evaluate_kernel.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int Fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define CSE_HIP(call)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return Fail(CSE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct KindShape {
+  int nr, nb, s0, s1, data;
+};
+
+bool ShapeOf(int kind, KindShape* k) {
+  switch (kind) {
+    case CSE_FUNCTOR_SNAVELY_2_9_3: *k = {2, 2, 9, 3, 2}; return true;
+    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3: *k = {2, 2, 7, 3, 2}; return true;
+    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3: *k = {2, 2, 10, 3, 2}; return true;
+    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3: *k = {3, 1, 3, 0, 3}; return true;
+    default: return false;
+  }
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    if (count == 0) return CSE_OK;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+      p = nullptr;
+      return Fail(CSE_ERR_OOM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed");
+    }
+    n = count;
+    return CSE_OK;
+  }
+  int upload(const T* h, size_t count, hipStream_t s) {
+    int rc = alloc(count);
+    if (rc) return rc;
+    if (count && hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess)
+      return Fail(CSE_ERR_HIP, "hipMemcpyAsync H2D failed");
+    return CSE_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct Group {
+  int kind = 0;
+  KindShape shape{};
+  cse_loss loss{};
+  int64_t n = 0;
+  bool affine = false;
+  int64_t partial_offset = 0;
+  int64_t num_wg = 0;
+  DevBuf<int32_t> ids;
+  DevBuf<double> data;
+  DevBuf<int64_t> gindex;  // only when not contiguous
+  int64_t first = 0;
+  // affine parameters
+  int64_t state_base[2] = {0, 0};
+  int64_t delta_base[2] = {0, 0};
+  int64_t res_base = 0;
+  int64_t jac_base[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  int64_t jac_stride[2] = {0, 0};
+};
+
+using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
+
+template <class K, int L, bool J, bool A>
+void LaunchT(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateGroupKernel<K, L, J, A>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
+}
+
+template <class K, int L>
+LaunchFn PickJA(bool jac, bool affine) {
+  if (jac) return affine ? &LaunchT<K, L, true, true> : &LaunchT<K, L, true, false>;
+  return affine ? &LaunchT<K, L, false, true> : &LaunchT<K, L, false, false>;
+}
+
+template <class K>
+LaunchFn PickL(int loss, bool jac, bool affine) {
+  switch (loss) {
+    case CSE_LOSS_HUBER: return PickJA<K, cse::kLossHuber>(jac, affine);
+    case CSE_LOSS_CAUCHY: return PickJA<K, cse::kLossCauchy>(jac, affine);
+    default: return PickJA<K, cse::kLossTrivial>(jac, affine);
+  }
+}
+
+LaunchFn Pick(int kind, int loss, bool jac, bool affine) {
+  switch (kind) {
+    case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, affine);
+    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3:
+      return PickL<cse::SnavelyNoDistortionKind>(loss, jac, affine);
+    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3:
+      return PickL<cse::SnavelyQuaternionKind>(loss, jac, affine);
+    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3:
+      return PickL<cse::PointDisplacementKind>(loss, jac, affine);
+    default: return nullptr;
+  }
+}
+
+}  // namespace
+
+struct cse_evaluator {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  cse_options opts{};
+  int64_t num_parameter_blocks = 0, num_parameters = 0, num_effective = 0, num_constant = 0;
+  int64_t num_residual_blocks = 0, num_residuals = 0, num_jacobian_values = 0;
+  int64_t num_plus_jacobian_values = 0;
+  bool has_layout = false;
+  bool jac_covered = true;  // every Jacobian value is written by some block
+  bool res_covered = true;
+  int64_t bytes_jac = 0, bytes_res = 0;
+  std::vector<Group> groups;
+  int64_t total_wg = 0;
+  bool any_general = false;
+  DevBuf<cse::PbDev> pbs;
+  DevBuf<double> cstate, plus_jac;
+  DevBuf<int64_t> res_layout, jac_layout, jac_offsets;
+  DevBuf<double> partials;
+  DevBuf<int> status;  // [0] running flag, [1] last status
+  // Host-path buffers (allocated on first use).
+  DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
+  int* status_host = nullptr;  // pinned
+  // Profiling: one (start, stop) event pair per evaluation around its
+  // group kernels, folded lazily so timing never stalls the launch queue.
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
+  double last_ms = 0.0, total_ms = 0.0;
+  int64_t launches = 0;
+};
+
+namespace {
+
+int Validate(const cse_problem_desc* d) {
+  if (!d) return Fail(CSE_ERR_INVALID, "null descriptor");
+  if (d->abi_version != CSE_ABI_VERSION)
+    return Fail(CSE_ERR_INVALID, "abi_version mismatch: descriptor " +
+                                     std::to_string(d->abi_version) + ", library " +
+                                     std::to_string(CSE_ABI_VERSION));
+  if (d->num_groups < 0 || (d->num_groups > 0 && !d->groups))
+    return Fail(CSE_ERR_INVALID, "bad groups");
+  if (d->num_parameter_blocks < 0 || (d->num_parameter_blocks > 0 && !d->parameter_blocks))
+    return Fail(CSE_ERR_INVALID, "bad parameter blocks");
+  for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
+    const cse_parameter_block& pb = d->parameter_blocks[b];
+    if (pb.size <= 0 || pb.tangent_size < 0 || pb.tangent_size > pb.size)
+      return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) + " has bad size");
+    const int64_t lim = pb.is_constant ? d->num_constant_parameters : d->num_parameters;
+    if (pb.state_offset < 0 || pb.state_offset + pb.size > lim)
+      return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) + " state out of range");
+    if (!pb.is_constant && (pb.delta_offset < 0 ||
+                            pb.delta_offset + pb.tangent_size > d->num_effective_parameters))
+      return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) + " delta out of range");
+    if (pb.plus_jacobian_offset >= 0 &&
+        pb.plus_jacobian_offset + (int64_t)pb.size * pb.tangent_size > d->num_plus_jacobian_values)
+      return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) +
+                                       " plus jacobian out of range");
+  }
+  if (d->num_constant_parameters > 0 && !d->constant_state)
+    return Fail(CSE_ERR_INVALID, "constant_state missing");
+  if (d->num_plus_jacobian_values > 0 && !d->plus_jacobians)
+    return Fail(CSE_ERR_INVALID, "plus_jacobians missing");
+  if (d->num_residual_blocks < 0 || !d->residual_layout)
+    return Fail(CSE_ERR_INVALID, "residual_layout missing");
+  return CSE_OK;
+}
+
+// Is the group table-free?  See evaluate_kernel.hpp for the two shapes.
+bool DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const KindShape& k,
+                  Group* G) {
+  const int64_t n = g.num_blocks;
+  if (n == 0) return false;
+  auto gidx = [&](int64_t i) {
+    return g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
+  };
+  const int sizes[2] = {k.s0, k.s1};
+  // Parameters: active, no manifold, state/delta offsets affine in the id.
+  for (int j = 0; j < k.nb; ++j) {
+    const int32_t id0 = g.parameter_block_ids[j];
+    const cse_parameter_block& pb0 = d->parameter_blocks[id0];
+    G->state_base[j] = pb0.state_offset - (int64_t)sizes[j] * id0;
+    G->delta_base[j] = pb0.delta_offset - (int64_t)sizes[j] * id0;
+  }
+  for (int64_t i = 0; i < n; ++i)
+    for (int j = 0; j < k.nb; ++j) {
+      const int32_t id = g.parameter_block_ids[i * k.nb + j];
+      const cse_parameter_block& pb = d->parameter_blocks[id];
+      if (pb.is_constant || pb.plus_jacobian_offset >= 0 || pb.tangent_size != sizes[j] ||
+          pb.size != sizes[j])
+        return false;
+      if (pb.state_offset != G->state_base[j] + (int64_t)sizes[j] * id) return false;
+      if (pb.delta_offset != G->delta_base[j] + (int64_t)sizes[j] * id) return false;
+    }
+  // Residuals.
+  G->res_base = d->residual_layout[gidx(0)];
+  for (int64_t i = 0; i < n; ++i)
+    if (d->residual_layout[gidx(i)] != G->res_base + (int64_t)k.nr * i) return false;
+  // Jacobian rows.
+  if (!d->jacobian_per_residual_layout || !d->jacobian_per_residual_offsets) return true;
+  const int64_t* L = d->jacobian_per_residual_layout;
+  const int64_t* O = d->jacobian_per_residual_offsets;
+  for (int j = 0; j < k.nb; ++j)
+    for (int r = 0; r < k.nr; ++r) G->jac_base[j][r] = O[L[gidx(0)] + j * k.nr + r];
+  for (int j = 0; j < k.nb; ++j)
+    G->jac_stride[j] = n > 1 ? O[L[gidx(1)] + j * k.nr] - G->jac_base[j][0] : (int64_t)k.nr * sizes[j];
+  for (int64_t i = 0; i < n; ++i)
+    for (int j = 0; j < k.nb; ++j)
+      for (int r = 0; r < k.nr; ++r)
+        if (O[L[gidx(i)] + j * k.nr + r] != G->jac_base[j][r] + G->jac_stride[j] * i) return false;
+  const int N = k.s0 + k.s1;
+  // Shape 1: packed cells (BlockSparseMatrix).
+  bool packed = true;
+  for (int j = 0; j < k.nb; ++j) {
+    if (G->jac_stride[j] != (int64_t)k.nr * sizes[j]) packed = false;
+    for (int r = 0; r < k.nr; ++r)
+      if (G->jac_base[j][r] != G->jac_base[j][0] + (int64_t)r * sizes[j]) packed = false;
+  }
+  if (packed && !(G->jac_stride[0] == (int64_t)k.nr * N && k.nb > 1)) return true;
+  // Shape 2: interleaved rows (CompressedRowSparseMatrix): every slot has
+  // stride kR*N, row r of the block starts at row0 + r*N and each slot sits
+  // at a fixed column position inside the row, the slots tiling [0, N).
+  int64_t row0 = G->jac_base[0][0];
+  for (int j = 0; j < k.nb; ++j) row0 = std::min(row0, G->jac_base[j][0]);
+  bool cover[32] = {false};
+  for (int j = 0; j < k.nb; ++j) {
+    if (G->jac_stride[j] != (int64_t)k.nr * N) return false;
+    const int64_t col = G->jac_base[j][0] - row0;
+    if (col < 0 || col + sizes[j] > N) return false;
+    for (int c = 0; c < sizes[j]; ++c) {
+      if (cover[col + c]) return false;
+      cover[col + c] = true;
+    }
+    for (int r = 0; r < k.nr; ++r)
+      if (G->jac_base[j][r] != row0 + (int64_t)r * N + col) return false;
+  }
+  return true;
+}
+
+cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double* res,
+                        double* jac, double* grad) {
+  cse::GroupArgs a{};
+  a.n = G.n;
+  a.ids = G.ids.p;
+  a.data = G.data.p;
+  a.state = state;
+  a.cstate = ev->cstate.p;
+  a.pbs = ev->pbs.p;
+  a.plus_jacobians = ev->plus_jac.p;
+  for (int j = 0; j < 2; ++j) {
+    a.state_base[j] = G.state_base[j];
+    a.delta_base[j] = G.delta_base[j];
+    a.jac_stride[j] = G.jac_stride[j];
+    for (int r = 0; r < 3; ++r) a.jac_base[j][r] = G.jac_base[j][r];
+  }
+  a.res_base = G.res_base;
+  a.gindex = G.gindex.p;
+  a.first = G.first;
+  a.residual_layout = ev->res_layout.p;
+  a.jac_layout = ev->jac_layout.p;
+  a.jac_offsets = ev->jac_offsets.p;
+  a.residuals = res;
+  a.jacobian = jac;
+  a.gradient = grad;
+  a.partials = ev->partials.p + G.partial_offset;
+  a.status = ev->status.p;
+  a.loss.a = G.loss.a;
+  a.loss.scale = G.loss.scale;
+  a.loss.scaled = G.loss.scaled;
+  a.apply_loss = ev->opts.apply_loss_function;
+  a.check_finite = ev->opts.check_finite;
+  return a;
+}
+
+int FoldTiming(cse_evaluator* ev) {
+  for (auto& pr : ev->pending) {
+    float ms = 0.f;
+    CSE_HIP(hipEventSynchronize(pr.second));
+    CSE_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+    ev->last_ms = ms;
+    ev->total_ms += ms;
+    ev->launches += 1;
+    ev->pool.push_back(pr);
+  }
+  ev->pending.clear();
+  return CSE_OK;
+}
+
+// Enqueue one evaluation on ev->stream.
+int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_res,
+            double* d_grad, double* d_jac) {
+  if (d_jac && !ev->has_layout)
+    return Fail(CSE_ERR_INVALID, "Jacobian requested but the descriptor had no Jacobian layout");
+  const bool jets = d_jac || d_grad;
+  std::pair<hipEvent_t, hipEvent_t> timing{nullptr, nullptr};
+  if (ev->opts.profile) {
+    if (ev->pool.empty()) {
+      CSE_HIP(hipEventCreate(&timing.first));
+      CSE_HIP(hipEventCreate(&timing.second));
+    } else {
+      timing = ev->pool.back();
+      ev->pool.pop_back();
+    }
+    if (ev->pending.size() > 4096) {
+      int rc = FoldTiming(ev);
+      if (rc) return rc;
+    }
+  }
+  if (d_grad && ev->num_effective > 0)
+    CSE_HIP(hipMemsetAsync(d_grad, 0, ev->num_effective * sizeof(double), ev->stream));
+  if (d_jac && !ev->jac_covered && ev->num_jacobian_values > 0)
+    CSE_HIP(hipMemsetAsync(d_jac, 0, ev->num_jacobian_values * sizeof(double), ev->stream));
+  if (d_res && !ev->res_covered && ev->num_residuals > 0)
+    CSE_HIP(hipMemsetAsync(d_res, 0, ev->num_residuals * sizeof(double), ev->stream));
+  for (size_t g = 0; g < ev->groups.size(); ++g) {
+    Group& G = ev->groups[g];
+    if (G.n == 0) continue;
+    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.affine);
+    if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
+    const cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, d_grad);
+    if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
+    fn(a, G.num_wg, ev->stream);
+    CSE_HIP(hipGetLastError());
+  }
+  if (timing.first) {
+    if (ev->groups.empty()) CSE_HIP(hipEventRecord(timing.first, ev->stream));
+    CSE_HIP(hipEventRecord(timing.second, ev->stream));
+    ev->pending.push_back(timing);
+  }
+  hipLaunchKernelGGL(cse::FinalizeKernel, dim3(1), dim3(1024), 0, ev->stream,
+                     (const double*)ev->partials.p, ev->total_wg, d_cost, ev->status.p,
+                     ev->status.p + 1);
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void cse_default_options(cse_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->device = -1;
+  o->check_finite = 1;
+  o->apply_loss_function = 1;
+}
+
+const char* cse_last_error(void) { return g_last_error.c_str(); }
+
+int cse_abi_version(void) { return CSE_ABI_VERSION; }
+
+const char* cse_build_info(void) {
+  return "cse abi=1 target=gfx950 built " __DATE__ " " __TIME__;
+}
+
+int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evaluator** out) {
+  if (!out) return Fail(CSE_ERR_INVALID, "null out");
+  *out = nullptr;
+  int rc = Validate(d);
+  if (rc) return rc;
+  cse_evaluator* ev = new (std::nothrow) cse_evaluator();
+  if (!ev) return Fail(CSE_ERR_OOM, "host allocation failed");
+  if (options) ev->opts = *options; else cse_default_options(&ev->opts);
+  auto bail = [&](int code) { cse_destroy(ev); return code; };
+
+  if (ev->opts.device >= 0) {
+    if (hipSetDevice(ev->opts.device) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "hipSetDevice failed"));
+    ev->device = ev->opts.device;
+  } else {
+    if (hipGetDevice(&ev->device) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "no HIP device"));
+  }
+  if (ev->opts.stream) {
+    ev->stream = (hipStream_t)ev->opts.stream;
+  } else {
+    if (hipStreamCreateWithFlags(&ev->stream, hipStreamNonBlocking) != hipSuccess)
+      return bail(Fail(CSE_ERR_HIP, "hipStreamCreate failed"));
+    ev->own_stream = true;
+  }
+  hipStream_t s = ev->stream;
+  ev->num_parameter_blocks = d->num_parameter_blocks;
+  ev->num_parameters = d->num_parameters;
+  ev->num_effective = d->num_effective_parameters;
+  ev->num_constant = d->num_constant_parameters;
+  ev->num_residual_blocks = d->num_residual_blocks;
+  ev->num_residuals = d->num_residuals;
+  ev->num_jacobian_values = d->num_jacobian_values;
+  ev->num_plus_jacobian_values = d->num_plus_jacobian_values;
+  ev->has_layout = d->jacobian_per_residual_layout && d->jacobian_per_residual_offsets;
+
+  // Groups.
+  int64_t covered_res = 0, covered_jac = 0;
+  std::vector<char> seen(d->num_parameter_blocks, 0);
+  for (int gi = 0; gi < d->num_groups; ++gi) {
+    const cse_residual_group& g = d->groups[gi];
+    Group G;
+    if (!ShapeOf(g.functor_kind, &G.shape))
+      return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown functor kind " + std::to_string(g.functor_kind)));
+    if (g.loss.kind < CSE_LOSS_TRIVIAL || g.loss.kind > CSE_LOSS_CAUCHY)
+      return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown loss kind " + std::to_string(g.loss.kind)));
+    if (g.num_blocks < 0 || (g.num_blocks > 0 && (!g.parameter_block_ids || !g.functor_data)))
+      return bail(Fail(CSE_ERR_INVALID, "group " + std::to_string(gi) + " arrays missing"));
+    G.kind = g.functor_kind;
+    G.loss = g.loss;
+    G.n = g.num_blocks;
+    G.first = g.first_residual_block;
+    const KindShape& k = G.shape;
+    for (int64_t i = 0; i < g.num_blocks; ++i) {
+      const int64_t gidx = g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
+      if (gidx < 0 || gidx >= d->num_residual_blocks)
+        return bail(Fail(CSE_ERR_INVALID, "residual block index out of range in group " + std::to_string(gi)));
+      if (d->residual_layout[gidx] < 0 || d->residual_layout[gidx] + k.nr > d->num_residuals)
+        return bail(Fail(CSE_ERR_INVALID, "residual_layout out of range"));
+      covered_res += k.nr;
+      for (int j = 0; j < k.nb; ++j) {
+        const int32_t id = g.parameter_block_ids[i * k.nb + j];
+        if (id < 0 || id >= d->num_parameter_blocks)
+          return bail(Fail(CSE_ERR_INVALID, "parameter block id out of range in group " + std::to_string(gi)));
+        const int want = j == 0 ? k.s0 : k.s1;
+        const cse_parameter_block& pb = d->parameter_blocks[id];
+        if (pb.size != want)
+          return bail(Fail(CSE_ERR_INVALID, "parameter block size does not match the functor"));
+        if (!pb.is_constant) covered_jac += (int64_t)k.nr * pb.tangent_size;
+        if (!seen[id]) {
+          seen[id] = 1;
+          ev->bytes_jac += 8LL * pb.size;
+          ev->bytes_res += 8LL * pb.size;
+        }
+      }
+      if (ev->has_layout) {
+        const int64_t base = d->jacobian_per_residual_layout[gidx];
+        int na = 0;
+        for (int j = 0; j < k.nb; ++j)
+          if (!d->parameter_blocks[g.parameter_block_ids[i * k.nb + j]].is_constant) ++na;
+        if (base < 0 || base + (int64_t)na * k.nr > d->num_jacobian_per_residual_offsets)
+          return bail(Fail(CSE_ERR_INVALID, "jacobian_per_residual_layout out of range"));
+        int a = 0;
+        for (int j = 0; j < k.nb; ++j) {
+          const cse_parameter_block& pb = d->parameter_blocks[g.parameter_block_ids[i * k.nb + j]];
+          if (pb.is_constant) continue;
+          for (int r = 0; r < k.nr; ++r) {
+            const int64_t off = d->jacobian_per_residual_offsets[base + a * k.nr + r];
+            if (off < 0 || off + pb.tangent_size > d->num_jacobian_values)
+              return bail(Fail(CSE_ERR_INVALID, "jacobian offset out of range"));
+          }
+          ++a;
+        }
+      }
+    }
+    const int64_t per_block = 8LL * k.data + 4LL * k.nb + 8LL * k.nr;
+    ev->bytes_res += per_block * g.num_blocks;
+    ev->bytes_jac += per_block * g.num_blocks;
+    G.affine = !ev->opts.force_general_layout && DetectAffine(d, g, k, &G);
+    if (!G.affine) ev->any_general = true;
+    G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
+    G.partial_offset = ev->total_wg;
+    ev->total_wg += G.num_wg;
+    if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
+    if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
+    if (!G.affine && g.residual_block_index &&
+        (rc = G.gindex.upload(g.residual_block_index, (size_t)g.num_blocks, s)))
+      return bail(rc);
+    ev->groups.push_back(std::move(G));
+  }
+  ev->bytes_jac += 8LL * covered_jac;
+  ev->res_covered = covered_res == d->num_residuals;
+  ev->jac_covered = covered_jac == d->num_jacobian_values;
+
+  // Program-level device state.
+  if ((rc = ev->cstate.upload(d->constant_state, (size_t)d->num_constant_parameters, s))) return bail(rc);
+  if ((rc = ev->plus_jac.upload(d->plus_jacobians, (size_t)d->num_plus_jacobian_values, s))) return bail(rc);
+  if (ev->any_general) {
+    std::vector<cse::PbDev> pbs(d->num_parameter_blocks);
+    for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
+      const cse_parameter_block& pb = d->parameter_blocks[b];
+      pbs[b] = {pb.state_offset, pb.delta_offset, pb.plus_jacobian_offset, pb.tangent_size,
+                pb.is_constant};
+    }
+    if ((rc = ev->pbs.upload(pbs.data(), pbs.size(), s))) return bail(rc);
+    if ((rc = ev->res_layout.upload(d->residual_layout, (size_t)d->num_residual_blocks, s))) return bail(rc);
+    if (ev->has_layout) {
+      if ((rc = ev->jac_layout.upload(d->jacobian_per_residual_layout, (size_t)d->num_residual_blocks, s)))
+        return bail(rc);
+      if ((rc = ev->jac_offsets.upload(d->jacobian_per_residual_offsets,
+                                       (size_t)d->num_jacobian_per_residual_offsets, s)))
+        return bail(rc);
+    }
+  }
+  if ((rc = ev->partials.alloc(std::max<int64_t>(ev->total_wg, 1)))) return bail(rc);
+  if ((rc = ev->status.alloc(2))) return bail(rc);
+  if (hipMemsetAsync(ev->status.p, 0, 2 * sizeof(int), s) != hipSuccess)
+    return bail(Fail(CSE_ERR_HIP, "memset failed"));
+  if (hipHostMalloc(&ev->status_host, sizeof(int)) != hipSuccess)
+    return bail(Fail(CSE_ERR_HIP, "hipHostMalloc failed"));
+  if (hipStreamSynchronize(s) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "upload failed"));
+  *out = ev;
+  return CSE_OK;
+}
+
+int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost,
+                        double* d_residuals, double* d_gradient, double* d_jacobian_values) {
+  if (!ev || !d_cost) return Fail(CSE_ERR_INVALID, "null evaluator or cost");
+  if (ev->num_parameters > 0 && !d_state) return Fail(CSE_ERR_INVALID, "null state");
+  if (hipSetDevice(ev->device) != hipSuccess) return Fail(CSE_ERR_HIP, "hipSetDevice failed");
+  return Enqueue(ev, d_state, d_cost, d_residuals, d_gradient, d_jacobian_values);
+}
+
+int cse_wait(cse_evaluator* ev) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  CSE_HIP(hipMemcpyAsync(ev->status_host, ev->status.p + 1, sizeof(int), hipMemcpyDeviceToHost,
+                         ev->stream));
+  CSE_HIP(hipStreamSynchronize(ev->stream));
+  if (ev->opts.profile) {
+    int rc = FoldTiming(ev);
+    if (rc) return rc;
+  }
+  return *ev->status_host ? CSE_EVALUATION_FAILED : CSE_OK;
+}
+
+int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* residuals,
+                 double* gradient, double* jacobian_values) {
+  if (!ev || !cost) return Fail(CSE_ERR_INVALID, "null evaluator or cost");
+  if (ev->num_parameters > 0 && !state) return Fail(CSE_ERR_INVALID, "null state");
+  CSE_HIP(hipSetDevice(ev->device));
+  int rc;
+  if (!ev->h_state.p && (rc = ev->h_state.alloc(std::max<int64_t>(ev->num_parameters, 1)))) return rc;
+  if (!ev->h_cost.p && (rc = ev->h_cost.alloc(1))) return rc;
+  if (residuals && !ev->h_res.p && (rc = ev->h_res.alloc(std::max<int64_t>(ev->num_residuals, 1)))) return rc;
+  if (gradient && !ev->h_grad.p && (rc = ev->h_grad.alloc(std::max<int64_t>(ev->num_effective, 1)))) return rc;
+  if (jacobian_values && !ev->h_jac.p &&
+      (rc = ev->h_jac.alloc(std::max<int64_t>(ev->num_jacobian_values, 1))))
+    return rc;
+  if (ev->num_parameters > 0)
+    CSE_HIP(hipMemcpyAsync(ev->h_state.p, state, ev->num_parameters * sizeof(double),
+                           hipMemcpyHostToDevice, ev->stream));
+  rc = Enqueue(ev, ev->h_state.p, ev->h_cost.p, residuals ? ev->h_res.p : nullptr,
+               gradient ? ev->h_grad.p : nullptr, jacobian_values ? ev->h_jac.p : nullptr);
+  if (rc) return rc;
+  rc = cse_wait(ev);
+  if (rc < 0) return rc;
+  if (rc == CSE_EVALUATION_FAILED) return rc;
+  CSE_HIP(hipMemcpy(cost, ev->h_cost.p, sizeof(double), hipMemcpyDeviceToHost));
+  if (residuals && ev->num_residuals > 0)
+    CSE_HIP(hipMemcpy(residuals, ev->h_res.p, ev->num_residuals * sizeof(double), hipMemcpyDeviceToHost));
+  if (gradient && ev->num_effective > 0)
+    CSE_HIP(hipMemcpy(gradient, ev->h_grad.p, ev->num_effective * sizeof(double), hipMemcpyDeviceToHost));
+  if (jacobian_values && ev->num_jacobian_values > 0)
+    CSE_HIP(hipMemcpy(jacobian_values, ev->h_jac.p, ev->num_jacobian_values * sizeof(double),
+                      hipMemcpyDeviceToHost));
+  return CSE_OK;
+}
+
+int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->num_plus_jacobian_values == 0) return CSE_OK;
+  if (!plus_jacobians) return Fail(CSE_ERR_INVALID, "null plus_jacobians");
+  CSE_HIP(hipSetDevice(ev->device));
+  CSE_HIP(hipMemcpyAsync(ev->plus_jac.p, plus_jacobians, ev->num_plus_jacobian_values * sizeof(double),
+                         hipMemcpyHostToDevice, ev->stream));
+  CSE_HIP(hipStreamSynchronize(ev->stream));
+  return CSE_OK;
+}
+
+void cse_destroy(cse_evaluator* ev) {
+  if (!ev) return;
+  (void)hipSetDevice(ev->device);
+  if (ev->stream) (void)hipStreamSynchronize(ev->stream);
+  for (auto& G : ev->groups) {
+    G.ids.release();
+    G.data.release();
+    G.gindex.release();
+  }
+  ev->pbs.release();
+  ev->cstate.release();
+  ev->plus_jac.release();
+  ev->res_layout.release();
+  ev->jac_layout.release();
+  ev->jac_offsets.release();
+  ev->partials.release();
+  ev->status.release();
+  ev->h_state.release();
+  ev->h_cost.release();
+  ev->h_res.release();
+  ev->h_jac.release();
+  ev->h_grad.release();
+  if (ev->status_host) (void)hipHostFree(ev->status_host);
+  for (auto& pr : ev->pending) ev->pool.push_back(pr);
+  for (auto& pr : ev->pool) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (ev->own_stream && ev->stream) (void)hipStreamDestroy(ev->stream);
+  delete ev;
+}
+
+int cse_get_info(cse_evaluator* ev, cse_info* info) {
+  if (!ev || !info) return Fail(CSE_ERR_INVALID, "null argument");
+  std::memset(info, 0, sizeof(*info));
+  info->num_residual_blocks = ev->num_residual_blocks;
+  info->num_residuals = ev->num_residuals;
+  info->num_parameters = ev->num_parameters;
+  info->num_effective_parameters = ev->num_effective;
+  info->num_jacobian_values = ev->num_jacobian_values;
+  info->num_groups = (int32_t)ev->groups.size();
+  for (auto& G : ev->groups) info->num_affine_groups += G.affine ? 1 : 0;
+  info->device = ev->device;
+  info->bytes_jacobian_eval = ev->bytes_jac;
+  info->bytes_residual_eval = ev->bytes_res;
+  return CSE_OK;
+}
+
+int cse_kernel_stats(cse_evaluator* ev, double* last_ms, double* total_ms, int64_t* launches) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (!ev->opts.profile) return Fail(CSE_ERR_INVALID, "evaluator created without options.profile");
+  int rc = FoldTiming(ev);
+  if (rc) return rc;
+  if (last_ms) *last_ms = ev->last_ms;
+  if (total_ms) *total_ms = ev->total_ms;
+  if (launches) *launches = ev->launches;
+  return CSE_OK;
+}
+
+int cse_reset_kernel_stats(cse_evaluator* ev) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  int rc = FoldTiming(ev);
+  if (rc) return rc;
+  ev->last_ms = ev->total_ms = 0.0;
+  ev->launches = 0;
+  return CSE_OK;
+}
+
+}  // extern "C"

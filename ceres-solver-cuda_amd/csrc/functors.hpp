@@ -1,0 +1,150 @@
+// functors.hpp -- residual functors pre-instantiated in the gfx950 library.
+//
+// Each functor kind carries its shape (kNumResiduals, parameter block
+// sizes, functor-data size) as compile-time traits and one templated
+// Evaluate(data, params, residuals) written for T in {double, Jet<N>}, the
+// same contract as a Ceres AutoDiffCostFunction functor
+// (include/ceres/autodiff_cost_function.h:201-217).
+#ifndef CSE_FUNCTORS_HPP_
+#define CSE_FUNCTORS_HPP_
+
+#include "jet.hpp"
+
+namespace cse {
+
+// y = R(angle_axis) x  (include/ceres/rotation.h:830-899): Rodrigues away
+// from theta == 0, the first-order form R = I + hat(w) exactly at zero so
+// Jets still carry the right derivatives.
+template <typename T>
+CSE_HD void AngleAxisRotatePoint(const T aa[3], const T pt[3], T out[3]) {
+  const T theta = jhypot(aa[0], aa[1], aa[2]);
+  if (value_of(theta) != 0.0) {
+    T sintheta, costheta;
+    jsincos(theta, &sintheta, &costheta);
+    const T theta_inverse = T(1.0) / theta;
+    const T w[3] = {aa[0] * theta_inverse, aa[1] * theta_inverse, aa[2] * theta_inverse};
+    const T w_cross_pt[3] = {w[1] * pt[2] - w[2] * pt[1],
+                             w[2] * pt[0] - w[0] * pt[2],
+                             w[0] * pt[1] - w[1] * pt[0]};
+    const T tmp = (w[0] * pt[0] + w[1] * pt[1] + w[2] * pt[2]) * (T(1.0) - costheta);
+    out[0] = pt[0] * costheta + w_cross_pt[0] * sintheta + w[0] * tmp;
+    out[1] = pt[1] * costheta + w_cross_pt[1] * sintheta + w[1] * tmp;
+    out[2] = pt[2] * costheta + w_cross_pt[2] * sintheta + w[2] * tmp;
+  } else {
+    out[0] = pt[0] + (aa[1] * pt[2] - aa[2] * pt[1]);
+    out[1] = pt[1] + (aa[2] * pt[0] - aa[0] * pt[2]);
+    out[2] = pt[2] + (aa[0] * pt[1] - aa[1] * pt[0]);
+  }
+}
+
+// y = R(q) x for a not necessarily unit quaternion
+// (include/ceres/rotation.h:753-798).
+template <typename T>
+CSE_HD void QuaternionRotatePoint(const T q[4], const T pt[3], T out[3]) {
+  const T scale = T(1.0) / jsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const T u[4] = {scale * q[0], scale * q[1], scale * q[2], scale * q[3]};
+  T uv0 = u[2] * pt[2] - u[3] * pt[1];
+  T uv1 = u[3] * pt[0] - u[1] * pt[2];
+  T uv2 = u[1] * pt[1] - u[2] * pt[0];
+  uv0 += uv0;
+  uv1 += uv1;
+  uv2 += uv2;
+  out[0] = pt[0] + u[0] * uv0;
+  out[1] = pt[1] + u[0] * uv1;
+  out[2] = pt[2] + u[0] * uv2;
+  out[0] += u[2] * uv2 - u[3] * uv1;
+  out[1] += u[3] * uv0 - u[1] * uv2;
+  out[2] += u[1] * uv1 - u[2] * uv0;
+}
+
+// Pinhole camera with the Bundler sign convention, optional radial
+// distortion (examples/snavely_reprojection_error.h:58-93).
+template <bool kDistortion, typename T>
+CSE_HD void Project(const T p[3], const T& focal, const T* l, const double* obs, T* r) {
+  const T xp = -p[0] / p[2];
+  const T yp = -p[1] / p[2];
+  if constexpr (kDistortion) {
+    const T r2 = xp * xp + yp * yp;
+    const T distortion = 1.0 + r2 * (l[0] + l[1] * r2);
+    r[0] = focal * distortion * xp - obs[0];
+    r[1] = focal * distortion * yp - obs[1];
+  } else {
+    r[0] = focal * xp - obs[0];
+    r[1] = focal * yp - obs[1];
+  }
+}
+
+// SnavelyReprojectionError<2, 9, 3>: camera = {aa[3], t[3], f, l1, l2}.
+struct SnavelyKind {
+  static constexpr int kNumResiduals = 2;
+  static constexpr int kNumBlocks = 2;
+  static constexpr int kSize0 = 9, kSize1 = 3;
+  static constexpr int kDataSize = 2;
+  template <typename T>
+  static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
+    T p[3];
+    AngleAxisRotatePoint(camera, point, p);
+    p[0] += camera[3];
+    p[1] += camera[4];
+    p[2] += camera[5];
+    Project<true>(p, camera[6], camera + 7, obs, r);
+    return true;
+  }
+};
+
+// SnavelyReprojectionErrorNoRadialDistortion<2, 7, 3>
+// (internal/ceres/evaluator_cuda_test.cu.cc:112-150).
+struct SnavelyNoDistortionKind {
+  static constexpr int kNumResiduals = 2;
+  static constexpr int kNumBlocks = 2;
+  static constexpr int kSize0 = 7, kSize1 = 3;
+  static constexpr int kDataSize = 2;
+  template <typename T>
+  static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
+    T p[3];
+    AngleAxisRotatePoint(camera, point, p);
+    p[0] += camera[3];
+    p[1] += camera[4];
+    p[2] += camera[5];
+    Project<false>(p, camera[6], camera, obs, r);
+    return true;
+  }
+};
+
+// SnavelyReprojectionErrorWithQuaternions<2, 10, 3>: camera =
+// {q[4], t[3], f, l1, l2} (examples/snavely_reprojection_error.h:112-175).
+struct SnavelyQuaternionKind {
+  static constexpr int kNumResiduals = 2;
+  static constexpr int kNumBlocks = 2;
+  static constexpr int kSize0 = 10, kSize1 = 3;
+  static constexpr int kDataSize = 2;
+  template <typename T>
+  static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
+    T p[3];
+    QuaternionRotatePoint(camera, point, p);
+    p[0] += camera[4];
+    p[1] += camera[5];
+    p[2] += camera[6];
+    Project<true>(p, camera[7], camera + 8, obs, r);
+    return true;
+  }
+};
+
+// PointDisplacementError<3, 3> (internal/ceres/evaluator_cuda_test.cu.cc:84-110).
+struct PointDisplacementKind {
+  static constexpr int kNumResiduals = 3;
+  static constexpr int kNumBlocks = 1;
+  static constexpr int kSize0 = 3, kSize1 = 0;
+  static constexpr int kDataSize = 3;
+  template <typename T>
+  static CSE_HD bool Evaluate(const double* xyz, const T* point, const T*, T* r) {
+    r[0] = fabs(xyz[0]) - jabs(point[0]);
+    r[1] = fabs(xyz[1]) - jabs(point[1]);
+    r[2] = fabs(xyz[2]) - jabs(point[2]);
+    return true;
+  }
+};
+
+}  // namespace cse
+
+#endif  // CSE_FUNCTORS_HPP_

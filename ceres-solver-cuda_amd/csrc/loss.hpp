@@ -1,0 +1,108 @@
+// loss.hpp -- robust losses and the Triggs correction, fused into the
+// evaluate kernel.
+//
+// Losses: include/ceres/loss_function_cuda.h:62-150 (Trivial, Huber,
+// Cauchy, Scaled).  Correction: include/ceres/internal/corrector.h:82-213.
+#ifndef CSE_LOSS_HPP_
+#define CSE_LOSS_HPP_
+
+#include <cfloat>
+
+#include "jet.hpp"
+
+namespace cse {
+
+enum LossKind { kLossTrivial = 0, kLossHuber = 1, kLossCauchy = 2 };
+
+struct LossParams {
+  double a;
+  double scale;
+  int scaled;
+};
+
+// rho(s) = (rho0, rho1, rho2).
+template <int kLoss>
+CSE_HD void EvaluateLoss(const LossParams& lp, double s, double rho[3]) {
+  if constexpr (kLoss == kLossHuber) {
+    const double a = lp.a, b = a * a;
+    if (s > b) {
+      const double r = sqrt(s);
+      rho[0] = 2.0 * a * r - b;
+      rho[1] = fmax(DBL_MIN, a / r);
+      rho[2] = -rho[1] / (2.0 * s);
+    } else {
+      rho[0] = s;
+      rho[1] = 1.0;
+      rho[2] = 0.0;
+    }
+  } else if constexpr (kLoss == kLossCauchy) {
+    const double b = lp.a * lp.a;
+    const double c = 1.0 / b;
+    const double sum = 1.0 + s * c;
+    const double inv = 1.0 / sum;
+    rho[0] = b * log(sum);
+    rho[1] = fmax(DBL_MIN, inv);
+    rho[2] = -c * (inv * inv);
+  } else {
+    rho[0] = s;
+    rho[1] = 1.0;
+    rho[2] = 0.0;
+  }
+  if (lp.scaled) {
+    rho[0] *= lp.scale;
+    rho[1] *= lp.scale;
+    rho[2] *= lp.scale;
+  }
+}
+
+// Corrector: residuals *= sqrt(rho1)/(1-alpha); J = sqrt(rho1) (J -
+// alpha/|r|^2 r r^T J) where alpha solves 0.5 a^2 - a - rho2/rho1 |r|^2 = 0.
+// With rho2 <= 0 (every Huber outlier, every Cauchy point) alpha = 0 and
+// both reduce to scaling by sqrt(rho1).
+struct Corrector {
+  double sqrt_rho1;
+  double residual_scaling;
+  double alpha_sq_norm;
+
+  CSE_HD Corrector(double sq_norm, const double rho[3]) {
+    sqrt_rho1 = sqrt(rho[1]);
+    if (sq_norm == 0.0 || rho[2] <= 0.0) {
+      residual_scaling = sqrt_rho1;
+      alpha_sq_norm = 0.0;
+    } else {
+      const double D = 1.0 + 2.0 * sq_norm * rho[2] / rho[1];
+      const double alpha = 1.0 - sqrt(D);
+      residual_scaling = sqrt_rho1 / (1.0 - alpha);
+      alpha_sq_norm = alpha / sq_norm;
+    }
+  }
+
+  // J is kR x kCols row-major, corrected in place; r is uncorrected.
+  template <int kR, int kCols>
+  CSE_HD void CorrectJacobian(const double* r, double* J) const {
+    if (alpha_sq_norm == 0.0) {
+#pragma unroll
+      for (int i = 0; i < kR * kCols; ++i) J[i] *= sqrt_rho1;
+      return;
+    }
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+      double rtj = 0.0;
+#pragma unroll
+      for (int k = 0; k < kR; ++k) rtj += J[k * kCols + c] * r[k];
+#pragma unroll
+      for (int k = 0; k < kR; ++k)
+        J[k * kCols + c] = sqrt_rho1 * (J[k * kCols + c] - alpha_sq_norm * r[k] * rtj);
+    }
+  }
+
+  template <int kR>
+  CSE_HD void CorrectResiduals(double* r) const {
+#pragma unroll
+    for (int k = 0; k < kR; ++k) r[k] *= residual_scaling;
+  }
+};
+
+}  // namespace cse
+
+#endif  // CSE_LOSS_HPP_

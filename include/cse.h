@@ -1,0 +1,255 @@
+/*
+ * cse.h -- C ABI of the MI355X (gfx950) residual/Jacobian evaluator.
+ *
+ * "cse" = Ceres Solver Evaluator.  This is the drop-in boundary for the hot
+ * path of jwmak/ceres-solver-cuda: the per-residual-block autodiff evaluator
+ * behind ProblemCUDA.  Every entry point names the reference interface it
+ * replaces (paths relative to the reference checkout).
+ *
+ * Plain C: no exceptions cross the boundary, no torch/HIP types in the
+ * signatures (streams are passed as void*), every buffer is a pointer plus
+ * a size.  All functions return 0 on success, a positive status for a
+ * numerical failure (a residual block reported failure) and a negative
+ * status for a usage or HIP error; cse_last_error() then describes it.
+ *
+ * Threading: an evaluator is not thread-safe (the reference's
+ * RegisteredCUDAEvaluators is not either).  Distinct evaluators may be used
+ * from distinct threads.
+ */
+#ifndef CSE_H_
+#define CSE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CSE_ABI_VERSION 1
+
+/* Return codes. */
+#define CSE_OK 0
+#define CSE_EVALUATION_FAILED 1 /* a functor returned false / non-finite output */
+#define CSE_ERR_INVALID -1      /* malformed descriptor or arguments */
+#define CSE_ERR_HIP -2          /* HIP runtime error */
+#define CSE_ERR_OOM -3          /* device allocation failed */
+#define CSE_ERR_UNSUPPORTED -4  /* functor/loss/layout not available */
+
+/* Residual functors pre-instantiated in the library.  The reference
+ * compiles user functors header-only into the user's nvcc TU
+ * (include/ceres/problem_cuda.h:110-160); across a C ABI the functor is a
+ * kind plus per-block constants ("functor data").
+ *   kind                                  kR  blocks  data
+ *   SNAVELY_2_9_3                          2  9,3     obs_x, obs_y
+ *       examples/snavely_reprojection_error.h:54-105
+ *   SNAVELY_NO_DISTORTION_2_7_3            2  7,3     obs_x, obs_y
+ *       internal/ceres/evaluator_cuda_test.cu.cc:112-150
+ *   SNAVELY_QUATERNION_2_10_3              2  10,3    obs_x, obs_y
+ *       examples/snavely_reprojection_error.h:112-175
+ *   POINT_DISPLACEMENT_3_3                 3  3       x, y, z
+ *       internal/ceres/evaluator_cuda_test.cu.cc:84-110
+ */
+typedef enum cse_functor_kind {
+  CSE_FUNCTOR_SNAVELY_2_9_3 = 0,
+  CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3 = 1,
+  CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 = 2,
+  CSE_FUNCTOR_POINT_DISPLACEMENT_3_3 = 3
+} cse_functor_kind;
+
+/* LossFunctionCUDA variants, include/ceres/loss_function_cuda.h:62-150. */
+typedef enum cse_loss_kind {
+  CSE_LOSS_TRIVIAL = 0, /* TrivialLossCUDA (or nullptr, problem_cuda.h:146-160) */
+  CSE_LOSS_HUBER = 1,   /* HuberLossCUDA(a) */
+  CSE_LOSS_CAUCHY = 2   /* CauchyLossCUDA(a) */
+} cse_loss_kind;
+
+typedef struct cse_loss {
+  int32_t kind;   /* cse_loss_kind */
+  int32_t scaled; /* 1 = wrapped in ScaledLossCUDA(rho, scale) */
+  double a;       /* loss parameter a */
+  double scale;   /* ScaledLossCUDA factor */
+} cse_loss;
+
+/* One parameter block of the reduced Program; replaces ParameterBlockCUDA
+ * (include/ceres/internal/parameter_block_cuda.h:106-116) as filled by
+ * RegisteredCUDAEvaluators::SetupParameterBlocks
+ * (internal/ceres/registered_cuda_evaluators.cc:123-198). */
+typedef struct cse_parameter_block {
+  int32_t size;                 /* ambient size */
+  int32_t tangent_size;         /* == size without a manifold */
+  int32_t is_constant;          /* held constant: no Jacobian, no gradient */
+  int32_t reserved;
+  int64_t state_offset;         /* into state (active) / constant_state (constant) */
+  int64_t delta_offset;         /* into the gradient (active only) */
+  int64_t plus_jacobian_offset; /* into plus_jacobians (size x tangent row-major), -1 = none */
+} cse_parameter_block;
+
+/* All residual blocks of one (functor kind, loss) type; replaces one
+ * AutoDiffResidualBlockCUDAEvaluator<F, Loss, kR, Ns...> and its residual
+ * blocks (include/ceres/internal/autodiff_residual_block_cuda_evaluator.h:62-334,
+ * registered per std::type_index in problem_cuda.h:462-468).  The loss is
+ * uniform over the group (one loss object per type is what ProblemCUDA
+ * users register in practice; groups may be split to vary it). */
+typedef struct cse_residual_group {
+  int32_t functor_kind;               /* cse_functor_kind */
+  int32_t reserved;
+  cse_loss loss;
+  int64_t num_blocks;
+  /* Global residual block index (program order, ResidualBlock::index())
+   * of block i; NULL means first_residual_block + i. */
+  const int64_t* residual_block_index;
+  int64_t first_residual_block;
+  /* [num_blocks][num parameter blocks of the kind], program indices. */
+  const int32_t* parameter_block_ids;
+  /* [num_blocks][data size of the kind] functor constants. */
+  const double* functor_data;
+} cse_residual_group;
+
+/* The reduced Program plus the Jacobian layout the evaluator writes into:
+ * the arguments of RegisteredCUDAEvaluators::Init
+ * (internal/ceres/registered_cuda_evaluators.cc:226-280), with int64 offsets
+ * (the reference's int32 overflows past ~89M observations). */
+typedef struct cse_problem_desc {
+  int32_t abi_version; /* CSE_ABI_VERSION */
+  int32_t num_groups;
+  const cse_residual_group* groups;
+
+  int64_t num_parameter_blocks;
+  const cse_parameter_block* parameter_blocks;
+  int64_t num_parameters;           /* Program::NumParameters (state size) */
+  int64_t num_effective_parameters; /* Program::NumEffectiveParameters */
+  int64_t num_constant_parameters;  /* Program::NumConstantParameters */
+  const double* constant_state;     /* host, copied once (registered_cuda_evaluators.cc:237-248) */
+  int64_t num_plus_jacobian_values;
+  const double* plus_jacobians;     /* host; refresh with cse_set_plus_jacobians */
+
+  int64_t num_residual_blocks;
+  int64_t num_residuals;
+  /* ProgramEvaluatorCUDA::BuildResidualLayout (program_evaluator_cuda.h:159-170). */
+  const int64_t* residual_layout;
+  /* {BlockJacobianWriter,CompressedRowJacobianWriter}::CreateJacobianPerResidualLayout
+   * (block_jacobian_writer.cc:154-160, compressed_row_jacobian_writer.cc:240-300). */
+  const int64_t* jacobian_per_residual_layout;
+  const int64_t* jacobian_per_residual_offsets;
+  int64_t num_jacobian_per_residual_offsets;
+  int64_t num_jacobian_values; /* SparseMatrix::num_nonzeros() */
+} cse_problem_desc;
+
+typedef struct cse_options {
+  int32_t device;               /* HIP device ordinal; -1 = current device */
+  int32_t check_finite;         /* reject non-finite r/J (residual_block.cc:110-129) */
+  int32_t apply_loss_function;  /* Evaluator::EvaluateOptions::apply_loss_function */
+  int32_t force_general_layout; /* never take the affine fast path (testing) */
+  int32_t profile;              /* time every evaluate kernel with HIP events */
+  int32_t reserved;
+  void* stream;                 /* hipStream_t to run on; NULL = evaluator-owned stream */
+} cse_options;
+
+typedef struct cse_evaluator cse_evaluator;
+
+/* Fills *options with the defaults: device -1, check_finite 1,
+ * apply_loss_function 1, everything else 0. */
+void cse_default_options(cse_options* options);
+
+/* Replaces RegisteredCUDAEvaluators::Init + each
+ * AutoDiffResidualBlockCUDAEvaluator::Init (uploads topology, layouts and
+ * constants once).  The descriptor's host arrays are copied; they may be
+ * freed after the call. */
+int cse_create(const cse_problem_desc* desc, const cse_options* options,
+               cse_evaluator** out);
+
+/* Replaces RegisteredCUDAEvaluators::Evaluate
+ * (include/ceres/internal/registered_cuda_evaluators.h:75-79): host
+ * pointers, any output except cost may be NULL, synchronous.  Returns
+ * CSE_OK, CSE_EVALUATION_FAILED (Evaluate returning false) or an error. */
+int cse_evaluate(cse_evaluator* ev, const double* state, double* cost,
+                 double* residuals, double* gradient, double* jacobian_values);
+
+/* Device-resident variant (no host copies; the roofline path): all pointers
+ * are device pointers on the evaluator's device, d_cost is one double.
+ * Asynchronous on the evaluator's stream; call cse_wait for the status. */
+int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost,
+                        double* d_residuals, double* d_gradient,
+                        double* d_jacobian_values);
+
+/* Synchronises the evaluator's stream and returns the status of the most
+ * recent evaluation (CSE_OK / CSE_EVALUATION_FAILED) or an error. */
+int cse_wait(cse_evaluator* ev);
+
+/* Replaces RegisteredCUDAEvaluators::UpdatePlusJacobians
+ * (registered_cuda_evaluators.cc:105-121): host array of
+ * num_plus_jacobian_values doubles. */
+int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians);
+
+void cse_destroy(cse_evaluator* ev);
+
+/* Thread-local description of the last error. */
+const char* cse_last_error(void);
+
+typedef struct cse_info {
+  int64_t num_residual_blocks;
+  int64_t num_residuals;
+  int64_t num_parameters;
+  int64_t num_effective_parameters;
+  int64_t num_jacobian_values;
+  int32_t num_groups;
+  int32_t num_affine_groups;  /* groups on the table-free fast path */
+  int32_t device;
+  int32_t reserved;
+  /* Compulsory HBM bytes of one residual+Jacobian evaluation (SURVEY.md
+   * §8(d)): per block functor data + parameter ids + residuals + Jacobian
+   * values, plus each distinct parameter block read once. */
+  int64_t bytes_jacobian_eval;
+  int64_t bytes_residual_eval; /* same without the Jacobian values */
+} cse_info;
+
+int cse_get_info(cse_evaluator* ev, cse_info* info);
+
+/* Kernel time of the evaluate kernels (HIP events on the evaluator's
+ * stream, needs options.profile): last launch and running totals. */
+int cse_kernel_stats(cse_evaluator* ev, double* last_ms, double* total_ms,
+                     int64_t* launches);
+int cse_reset_kernel_stats(cse_evaluator* ev);
+
+/* Host-side layout builders for callers that do not have Ceres' writers
+ * (restating internal/ceres/block_jacobian_writer.cc:62-160 and
+ * compressed_row_jacobian_writer.cc:93-193,240-300).
+ *
+ * Inputs: parameter blocks (program order) and, per residual block in
+ * program order, its parameter block ids (CSR: param_begin[nrb+1]) and
+ * residual count.  Outputs the residual layout, per-residual layout and
+ * offsets (sized by the *_count queries) and the value count.  For CRS,
+ * crs_rows[num_residuals+1] and crs_cols[num_values] are optional. */
+int cse_block_sparse_layout(int64_t num_parameter_blocks,
+                            const cse_parameter_block* parameter_blocks,
+                            int64_t num_residual_blocks, const int64_t* param_begin,
+                            const int32_t* param_ids, const int32_t* num_residuals,
+                            int64_t num_eliminate_blocks, int64_t* residual_layout,
+                            int64_t* jacobian_per_residual_layout,
+                            int64_t* jacobian_per_residual_offsets,
+                            int64_t* num_jacobian_values);
+int cse_compressed_row_layout(int64_t num_parameter_blocks,
+                              const cse_parameter_block* parameter_blocks,
+                              int64_t num_residual_blocks, const int64_t* param_begin,
+                              const int32_t* param_ids, const int32_t* num_residuals,
+                              int64_t* residual_layout,
+                              int64_t* jacobian_per_residual_layout,
+                              int64_t* jacobian_per_residual_offsets,
+                              int64_t* num_jacobian_values, int64_t* crs_rows,
+                              int64_t* crs_cols);
+/* Number of jacobian_per_residual_offsets entries for either layout. */
+int64_t cse_layout_offsets_count(int64_t num_parameter_blocks,
+                                 const cse_parameter_block* parameter_blocks,
+                                 int64_t num_residual_blocks, const int64_t* param_begin,
+                                 const int32_t* param_ids, const int32_t* num_residuals);
+
+/* Library identification: ABI version and the gfx target it was built for. */
+int cse_abi_version(void);
+const char* cse_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CSE_H_ */

@@ -1,0 +1,48 @@
+"""Shared helpers for the GPU-vs-oracle parity tests.
+
+Tolerance (stated once, used everywhere): the reference's own parity
+criterion between its CPU and CUDA evaluators, Eigen isApprox with
+kTolerance = 1e-13 per output vector
+(internal/ceres/evaluator_cuda_test.cu.cc:61,426-440):
+    ||x - x_ref|| <= 1e-13 * min(||x||, ||x_ref||)
+and for the scalar cost |cost - cost_ref| <= 1e-12 * |cost_ref| (the
+reference uses EXPECT_NEAR 1e-13 absolute on a 6-block problem; summing
+millions of blocks in a different order needs a relative bound).
+"""
+import numpy as np
+
+TOL = 1e-13
+COST_RTOL = 1e-12
+
+
+def is_approx(x, y, tol=TOL):
+    x, y = np.ravel(x), np.ravel(y)
+    nx, ny = np.linalg.norm(x), np.linalg.norm(y)
+    if nx == 0 and ny == 0:
+        return True
+    return np.linalg.norm(x - y) <= tol * min(nx, ny)
+
+
+def max_rel_err(x, y, floor=1e-8):
+    x, y = np.ravel(x), np.ravel(y)
+    m = np.abs(y) > floor
+    if not m.any():
+        return 0.0
+    return float(np.max(np.abs(x[m] - y[m]) / np.abs(y[m])))
+
+
+def assert_parity(gpu, ref, what=""):
+    ok_g, cost_g, r_g, g_g, j_g = gpu
+    ok_r, cost_r, r_r, g_r, j_r = ref
+    assert ok_g == ok_r, (what, ok_g, ok_r)
+    if not ok_r:
+        return
+    assert abs(cost_g - cost_r) <= COST_RTOL * abs(cost_r) + 1e-300, (what, cost_g, cost_r)
+    for name, a, b in (("residuals", r_g, r_r), ("gradient", g_g, g_r), ("jacobian", j_g, j_r)):
+        if b is None:
+            continue
+        assert a is not None
+        assert a.shape == b.shape, (what, name)
+        assert np.isfinite(a).all(), (what, name)
+        assert is_approx(a, b), (what, name, np.linalg.norm(a - b) / np.linalg.norm(b),
+                                 max_rel_err(a, b))

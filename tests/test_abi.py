@@ -1,0 +1,72 @@
+"""The C ABI library loads and exports every symbol include/cse.h declares
+(no compute call: this runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "cse.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = set(re.findall(r"\b(cse_[a-z_]+)\s*\(", text))
+    return sorted(names)
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("cse_create", "cse_evaluate", "cse_evaluate_device", "cse_destroy",
+                     "cse_last_error", "cse_wait"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from ceres_amd import _cse
+    lib = ctypes.CDLL(_cse.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # ... and the Python binding declares a signature for each of them.
+    assert set(declared_functions()) == set(_cse.SIGNATURES)
+
+
+def test_abi_version_and_build_info():
+    from ceres_amd import _cse
+    L = _cse.lib()
+    assert L.cse_abi_version() == _cse.CSE_ABI_VERSION
+    assert b"gfx950" in L.cse_build_info()
+
+
+def test_struct_layouts_match_header():
+    """ctypes mirrors of the descriptor structs have the C sizes."""
+    from ceres_amd import _cse
+    assert ctypes.sizeof(_cse.cse_loss) == 24
+    assert ctypes.sizeof(_cse.cse_parameter_block) == 40
+    assert ctypes.sizeof(_cse.cse_residual_group) == 72
+    assert ctypes.sizeof(_cse.cse_options) == 32
+
+
+def test_create_rejects_bad_descriptors_without_a_gpu():
+    """Validation happens before any HIP call: malformed input fails with
+    CSE_ERR_INVALID and a message."""
+    from ceres_amd import _cse
+    L = _cse.lib()
+    h = ctypes.c_void_p()
+    assert L.cse_create(None, None, ctypes.byref(h)) == _cse.CSE_ERR_INVALID
+    d = _cse.cse_problem_desc()
+    d.abi_version = 999
+    assert L.cse_create(ctypes.byref(d), None, ctypes.byref(h)) == _cse.CSE_ERR_INVALID
+    assert "abi_version" in _cse.last_error()
+
+
+def test_no_cpu_fallback_in_the_product():
+    """The product package never imports the oracle or numpy math for the
+    evaluation itself."""
+    pkg = os.path.join(REPO, "ceres-solver-cuda_amd", "ceres_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "oracle" not in src.replace("oracle/", ""), f
