@@ -15,6 +15,8 @@
   cameras follow, residual blocks are grouped by point
   (reorder_program.cc:254-336).
 """
+import os
+
 import numpy as np
 
 from . import _cse
@@ -51,7 +53,25 @@ def project(cameras, points, cam_idx, pt_idx):
 
 def synthetic(num_cameras, num_points, num_observations, seed=0xCE2E5, outlier_fraction=0.05):
     """Returns (cameras[C,9], points[P,3], cam_idx[O], pt_idx[O], obs[O,2]) in
-    point-major order."""
+    point-major order.  If $CSE_BAL_CACHE names a directory, the arrays are
+    cached there (profiling runs regenerate the same problem many times)."""
+    cache = os.environ.get("CSE_BAL_CACHE")
+    if cache:
+        path = os.path.join(cache, f"bal_{num_cameras}_{num_points}_{num_observations}_"
+                                   f"{seed}_{outlier_fraction}.npz")
+        if os.path.exists(path):
+            with np.load(path) as z:
+                return z["cameras"], z["points"], z["cam_idx"], z["pt_idx"], z["obs"]
+        out = _synthetic(num_cameras, num_points, num_observations, seed, outlier_fraction)
+        os.makedirs(cache, exist_ok=True)
+        tmp = path + f".{os.getpid()}.npz"
+        np.savez(tmp, cameras=out[0], points=out[1], cam_idx=out[2], pt_idx=out[3], obs=out[4])
+        os.replace(tmp, path)
+        return out
+    return _synthetic(num_cameras, num_points, num_observations, seed, outlier_fraction)
+
+
+def _synthetic(num_cameras, num_points, num_observations, seed, outlier_fraction):
     C, P, O = int(num_cameras), int(num_points), int(num_observations)
     if O < P:
         raise ValueError("need at least one observation per point")

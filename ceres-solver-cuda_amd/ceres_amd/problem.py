@@ -299,10 +299,26 @@ class ProblemCUDA:
     def add_residual_block(self, kind, loss, data, *blocks):
         return self.add_residual_blocks(kind, loss, [blocks], [data])[0]
 
-    def program(self, group_by_type=True):
+    def program(self, group_by_type=True, reduce=True):
         """Program order = insertion order.  Blocks sharing (kind, loss) are
-        merged into one group, like the per-type evaluator registry."""
+        merged into one group, like the per-type evaluator registry.
+
+        reduce: drop residual blocks whose parameter blocks are all constant,
+        as Program::CreateReducedProgram does before evaluation
+        (program.cc RemoveFixedBlocks); their cost is the solver's fixed
+        cost, not the evaluator's."""
         groups = self._groups
+        const_flags = np.array(self._const, np.int32)
+        if reduce:
+            kept, nrb = [], 0
+            for g in groups:
+                live = ~np.all(const_flags[g.ids] != 0, axis=1)
+                if live.any():
+                    kept.append(ResidualGroup(g.kind, g.loss, g.ids[live], g.data[live], None, nrb))
+                    nrb += int(live.sum())
+            groups = kept
+        else:
+            nrb = self._nrb
         if group_by_type:
             merged = {}
             for g in groups:
@@ -325,7 +341,7 @@ class ProblemCUDA:
         cstate = np.concatenate([v for v, c in zip(values, const) if c] or [np.zeros(0)])
         pj = np.concatenate(self._pj) if self._pj else np.zeros(0)
         return Program(np.array(self._sizes, np.int32), np.array(self._tangent, np.int32), const,
-                       np.array(self._pj_off, np.int64), pj, groups, self._nrb, state, cstate)
+                       np.array(self._pj_off, np.int64), pj, groups, nrb, state, cstate)
 
 
 class Evaluator:
