@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -80,6 +81,7 @@ struct Group {
   cse_loss loss{};
   int64_t n = 0;
   bool affine = false;
+  int policy = 0;
   int64_t partial_offset = 0;
   int64_t num_wg = 0;
   DevBuf<int32_t> ids;
@@ -96,44 +98,110 @@ struct Group {
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
 
-template <class K, int L, bool J, bool A>
-void LaunchT(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateGroupKernel<K, L, J, A>), dim3((unsigned)num_wg),
+template <class K, int L, bool J>
+void LaunchGeneral(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateGroupKernel<K, L, J>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
+template <class K, int L, bool J, bool Crs, int Pf = 2, bool St = true, int Mw = 0>
+void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  if constexpr (Mw == 0) {
+    hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St>),
+                       dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((cse::EvaluateAffinePersistent<K, L, J, Crs, Pf, St, Mw>),
+                       dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
+  }
+}
+
+// Tuning variants of the hot kernel (Snavely, Huber/Trivial, BSM,
+// Jacobian), selected by $CSE_AFFINE_VARIANT: (prefetch, LDS staging,
+// min waves per SIMD).
+template <int L>
+LaunchFn SnavelyVariant(int v) {
+  using K = cse::SnavelyKind;
+  switch (v) {
+    case 1: return &LaunchAffine<K, L, true, false, 2, true, 3>;
+    case 2: return &LaunchAffine<K, L, true, false, 1, true, 0>;
+    case 3: return &LaunchAffine<K, L, true, false, 0, true, 0>;
+    case 4: return &LaunchAffine<K, L, true, false, 1, false, 0>;
+    case 5: return &LaunchAffine<K, L, true, false, 0, false, 0>;
+    case 6: return &LaunchAffine<K, L, true, false, 2, false, 0>;
+    case 7: return &LaunchAffine<K, L, true, false, 1, true, 4>;
+    case 8: return &LaunchAffine<K, L, true, false, -1, true, 0>;
+    case 9: return &LaunchAffine<K, L, true, false, -1, false, 0>;
+    default: return nullptr;
+  }
+}
+
+int AffineVariant() {
+  const char* e = getenv("CSE_AFFINE_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
+// Layout policy of a group: 0 = table, 1 = affine packed cells (BSM),
+// 2 = affine interleaved rows (CRS).
+enum Policy { kTable = 0, kAffinePacked = 1, kAffineCrs = 2 };
+
 template <class K, int L>
-LaunchFn PickJA(bool jac, bool affine) {
-  if (jac) return affine ? &LaunchT<K, L, true, true> : &LaunchT<K, L, true, false>;
-  return affine ? &LaunchT<K, L, false, true> : &LaunchT<K, L, false, false>;
+LaunchFn PickJP(bool jac, int policy) {
+  switch (policy) {
+    case kAffinePacked: return jac ? &LaunchAffine<K, L, true, false> : &LaunchAffine<K, L, false, false>;
+    case kAffineCrs: return jac ? &LaunchAffine<K, L, true, true> : &LaunchAffine<K, L, false, true>;
+    default: return jac ? &LaunchGeneral<K, L, true> : &LaunchGeneral<K, L, false>;
+  }
 }
 
 template <class K>
-LaunchFn PickL(int loss, bool jac, bool affine) {
+LaunchFn PickL(int loss, bool jac, int policy) {
   switch (loss) {
-    case CSE_LOSS_HUBER: return PickJA<K, cse::kLossHuber>(jac, affine);
-    case CSE_LOSS_CAUCHY: return PickJA<K, cse::kLossCauchy>(jac, affine);
-    default: return PickJA<K, cse::kLossTrivial>(jac, affine);
+    case CSE_LOSS_HUBER: return PickJP<K, cse::kLossHuber>(jac, policy);
+    case CSE_LOSS_CAUCHY: return PickJP<K, cse::kLossCauchy>(jac, policy);
+    default: return PickJP<K, cse::kLossTrivial>(jac, policy);
   }
 }
 
-LaunchFn Pick(int kind, int loss, bool jac, bool affine) {
+LaunchFn Pick(int kind, int loss, bool jac, int policy) {
+  const int v = AffineVariant();
+  if (v > 0 && kind == CSE_FUNCTOR_SNAVELY_2_9_3 && jac && policy == kAffinePacked) {
+    LaunchFn f = loss == CSE_LOSS_HUBER ? SnavelyVariant<cse::kLossHuber>(v)
+               : loss == CSE_LOSS_TRIVIAL ? SnavelyVariant<cse::kLossTrivial>(v) : nullptr;
+    if (f) return f;
+  }
   switch (kind) {
-    case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, affine);
+    case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, policy);
     case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3:
-      return PickL<cse::SnavelyNoDistortionKind>(loss, jac, affine);
+      return PickL<cse::SnavelyNoDistortionKind>(loss, jac, policy);
     case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3:
-      return PickL<cse::SnavelyQuaternionKind>(loss, jac, affine);
+      return PickL<cse::SnavelyQuaternionKind>(loss, jac, policy);
     case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3:
-      return PickL<cse::PointDisplacementKind>(loss, jac, affine);
+      return PickL<cse::PointDisplacementKind>(loss, jac, policy);
     default: return nullptr;
   }
+}
+
+// Workgroups per CU of the persistent kernel: LDS-bound (4 waves per
+// workgroup, 64 lanes x staged doubles each) unless overridden by
+// $CSE_WG_PER_CU for tuning.
+int PersistentWgPerCu(const KindShape& k, int policy) {
+  if (const char* e = getenv("CSE_WG_PER_CU")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+    if (v == 0) return 1 << 20;  // one chunk per wave: not persistent
+  }
+  if (AffineVariant() >= 8) return 1 << 20;  // the non-persistent variants
+  const int lane_doubles = policy == kAffineCrs ? k.nr * (k.s0 + k.s1)
+                                                : k.nr * std::max(k.s0, k.s1);
+  const int lds = cse::kWavesPerBlock * cse::kWave * lane_doubles * 8 + 64;
+  return std::max(1, std::min(8, (160 * 1024) / lds));
 }
 
 }  // namespace
 
 struct cse_evaluator {
   int device = 0;
+  int num_cus = 256;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   cse_options opts{};
@@ -198,11 +266,12 @@ int Validate(const cse_problem_desc* d) {
   return CSE_OK;
 }
 
-// Is the group table-free?  See evaluate_kernel.hpp for the two shapes.
-bool DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const KindShape& k,
+// Is the group table-free?  Returns the Policy (see evaluate_kernel.hpp
+// for the two affine shapes).
+int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const KindShape& k,
                   Group* G) {
   const int64_t n = g.num_blocks;
-  if (n == 0) return false;
+  if (n == 0) return kTable;
   auto gidx = [&](int64_t i) {
     return g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
   };
@@ -220,16 +289,16 @@ bool DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const 
       const cse_parameter_block& pb = d->parameter_blocks[id];
       if (pb.is_constant || pb.plus_jacobian_offset >= 0 || pb.tangent_size != sizes[j] ||
           pb.size != sizes[j])
-        return false;
-      if (pb.state_offset != G->state_base[j] + (int64_t)sizes[j] * id) return false;
-      if (pb.delta_offset != G->delta_base[j] + (int64_t)sizes[j] * id) return false;
+        return kTable;
+      if (pb.state_offset != G->state_base[j] + (int64_t)sizes[j] * id) return kTable;
+      if (pb.delta_offset != G->delta_base[j] + (int64_t)sizes[j] * id) return kTable;
     }
   // Residuals.
   G->res_base = d->residual_layout[gidx(0)];
   for (int64_t i = 0; i < n; ++i)
-    if (d->residual_layout[gidx(i)] != G->res_base + (int64_t)k.nr * i) return false;
+    if (d->residual_layout[gidx(i)] != G->res_base + (int64_t)k.nr * i) return kTable;
   // Jacobian rows.
-  if (!d->jacobian_per_residual_layout || !d->jacobian_per_residual_offsets) return true;
+  if (!d->jacobian_per_residual_layout || !d->jacobian_per_residual_offsets) return kAffinePacked;
   const int64_t* L = d->jacobian_per_residual_layout;
   const int64_t* O = d->jacobian_per_residual_offsets;
   for (int j = 0; j < k.nb; ++j)
@@ -239,7 +308,7 @@ bool DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const 
   for (int64_t i = 0; i < n; ++i)
     for (int j = 0; j < k.nb; ++j)
       for (int r = 0; r < k.nr; ++r)
-        if (O[L[gidx(i)] + j * k.nr + r] != G->jac_base[j][r] + G->jac_stride[j] * i) return false;
+        if (O[L[gidx(i)] + j * k.nr + r] != G->jac_base[j][r] + G->jac_stride[j] * i) return kTable;
   const int N = k.s0 + k.s1;
   // Shape 1: packed cells (BlockSparseMatrix).
   bool packed = true;
@@ -248,7 +317,7 @@ bool DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const 
     for (int r = 0; r < k.nr; ++r)
       if (G->jac_base[j][r] != G->jac_base[j][0] + (int64_t)r * sizes[j]) packed = false;
   }
-  if (packed && !(G->jac_stride[0] == (int64_t)k.nr * N && k.nb > 1)) return true;
+  if (packed && !(G->jac_stride[0] == (int64_t)k.nr * N && k.nb > 1)) return kAffinePacked;
   // Shape 2: interleaved rows (CompressedRowSparseMatrix): every slot has
   // stride kR*N, row r of the block starts at row0 + r*N and each slot sits
   // at a fixed column position inside the row, the slots tiling [0, N).
@@ -256,17 +325,17 @@ bool DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const 
   for (int j = 0; j < k.nb; ++j) row0 = std::min(row0, G->jac_base[j][0]);
   bool cover[32] = {false};
   for (int j = 0; j < k.nb; ++j) {
-    if (G->jac_stride[j] != (int64_t)k.nr * N) return false;
+    if (G->jac_stride[j] != (int64_t)k.nr * N) return kTable;
     const int64_t col = G->jac_base[j][0] - row0;
-    if (col < 0 || col + sizes[j] > N) return false;
+    if (col < 0 || col + sizes[j] > N) return kTable;
     for (int c = 0; c < sizes[j]; ++c) {
-      if (cover[col + c]) return false;
+      if (cover[col + c]) return kTable;
       cover[col + c] = true;
     }
     for (int r = 0; r < k.nr; ++r)
-      if (G->jac_base[j][r] != row0 + (int64_t)r * N + col) return false;
+      if (G->jac_base[j][r] != row0 + (int64_t)r * N + col) return kTable;
   }
-  return true;
+  return kAffineCrs;
 }
 
 cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double* res,
@@ -347,7 +416,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
   for (size_t g = 0; g < ev->groups.size(); ++g) {
     Group& G = ev->groups[g];
     if (G.n == 0) continue;
-    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.affine);
+    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy);
     if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
     const cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, d_grad);
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
@@ -402,6 +471,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   } else {
     if (hipGetDevice(&ev->device) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "no HIP device"));
   }
+  if (hipDeviceGetAttribute(&ev->num_cus, hipDeviceAttributeMultiprocessorCount, ev->device) !=
+      hipSuccess)
+    return bail(Fail(CSE_ERR_HIP, "hipDeviceGetAttribute failed"));
   if (ev->opts.stream) {
     ev->stream = (hipStream_t)ev->opts.stream;
   } else {
@@ -482,9 +554,17 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     const int64_t per_block = 8LL * k.data + 4LL * k.nb + 8LL * k.nr;
     ev->bytes_res += per_block * g.num_blocks;
     ev->bytes_jac += per_block * g.num_blocks;
-    G.affine = !ev->opts.force_general_layout && DetectAffine(d, g, k, &G);
+    G.policy = ev->opts.force_general_layout ? kTable : DetectAffine(d, g, k, &G);
+    G.affine = G.policy != kTable;
     if (!G.affine) ev->any_general = true;
-    G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
+    if (G.affine) {
+      const int64_t chunks = (g.num_blocks + cse::kWave - 1) / cse::kWave;
+      const int64_t cap = (int64_t)ev->num_cus * PersistentWgPerCu(k, G.policy);
+      G.num_wg = std::max<int64_t>(1, std::min<int64_t>((chunks + cse::kWavesPerBlock - 1) /
+                                                            cse::kWavesPerBlock, cap));
+    } else {
+      G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
+    }
     G.partial_offset = ev->total_wg;
     ev->total_wg += G.num_wg;
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);

@@ -1,4 +1,4 @@
-// evaluate_kernel.hpp -- the fused residual/Jacobian/loss/cost kernel.
+// evaluate_kernel.hpp -- the fused residual/Jacobian/loss/cost kernels.
 //
 // One wavefront lane owns one residual block (the reference's
 // EvaluateKernel, include/ceres/internal/cuda_evaluator_kernel.h:297-422,
@@ -6,22 +6,28 @@
 //   gather parameters -> Jet autodiff of the functor -> plus-Jacobian
 //   product (manifolds) -> loss rho(|r|^2) and Corrector on J then r ->
 //   residual/Jacobian stores -> gradient J^T r -> cost into a per-workgroup
-//   partial (summed deterministically by cse_finalize_kernel).
+//   partial (summed deterministically by FinalizeKernel).
 //
 // Two layout policies, chosen per residual group on the host:
-//   kAffine = true   table-free: block i of the group writes its residuals
-//                    at res_base + kR*i and row k of slot j at
-//                    jac_base[j][k] + jac_stride[j]*i, and reads parameter
-//                    block `id` at state_base[j] + size_j*id.  This is what
-//                    BlockJacobianWriter and CompressedRowJacobianWriter
-//                    produce for Schur-ordered BAL problems; the kernel then
-//                    reads only 8 B of ids + functor data per block.
-//   kAffine = false  the reference's offset tables (residual_layout,
-//                    jacobian_per_residual_layout/offsets, per-block
-//                    parameter-block records): any layout, constant blocks,
-//                    manifolds.
-// Wide outputs of the affine path are staged through LDS so each wave
-// writes its contiguous output segments with 16-byte-per-lane stores.
+//   affine  table-free: block i of the group writes its residuals at
+//           res_base + kR*i and row k of slot j at jac_base[j][k] +
+//           jac_stride[j]*i, and reads parameter block `id` of slot j at
+//           state_base[j] + size_j*id.  This is what BlockJacobianWriter and
+//           CompressedRowJacobianWriter produce for Schur-ordered BAL
+//           problems: per block the kernel reads only 8 B of ids and the
+//           functor data.  Kernel: EvaluateAffinePersistent.
+//   table   the reference's offset tables (residual_layout,
+//           jacobian_per_residual_layout/offsets, per-block parameter-block
+//           records): any layout, constant blocks, manifolds.
+//           Kernel: EvaluateGroupKernel<..., kAffine = false>.
+//
+// EvaluateAffinePersistent is the hot path.  It is sized to the chip (a
+// fixed number of workgroups per CU), each wave walks 64-block chunks and
+// software-pipelines them: while chunk c is differentiated, the parameter
+// gathers of chunk c+1 and the ids of chunk c+2 are in flight, so the two
+// dependent HBM round trips (ids -> camera/point) never stall a wave.  Its
+// outputs are staged through LDS so every wave writes its contiguous output
+// segments with 16-byte-per-lane stores (1 KiB per wave instruction).
 #ifndef CSE_EVALUATE_KERNEL_HPP_
 #define CSE_EVALUATE_KERNEL_HPP_
 
@@ -35,8 +41,9 @@ namespace cse {
 
 constexpr int kBlockThreads = 256;
 constexpr int kWave = 64;
+constexpr int kWavesPerBlock = kBlockThreads / kWave;
 
-// Device copy of a parameter block (general path).
+// Device copy of a parameter block (table path).
 struct PbDev {
   int64_t state_offset;
   int64_t delta_offset;
@@ -76,6 +83,17 @@ struct GroupArgs {
   int check_finite;
 };
 
+template <class K>
+struct KindTraits {
+  static constexpr int NR = K::kNumResiduals;
+  static constexpr int NB = K::kNumBlocks;
+  static constexpr int S0 = K::kSize0;
+  static constexpr int S1 = K::kSize1;
+  static constexpr int S1p = S1 > 0 ? S1 : 1;
+  static constexpr int N = S0 + S1;
+  static constexpr int D = K::kDataSize;
+};
+
 // Any of x[0..n) NaN or infinite?  An integer test on the exponent field:
 // the TU is compiled with -ffinite-math-only, which would fold isfinite().
 template <int kCount>
@@ -89,35 +107,32 @@ CSE_HD bool AnyNonFinite(const double* x) {
   return m == 0x7ff00000u;
 }
 
-CSE_HD int64_t GlobalIndex(const GroupArgs& a, int64_t i) {
-  return a.gindex ? a.gindex[i] : a.first + i;
-}
-
-// Deterministic workgroup sum: xor-butterfly inside each wave, then waves
-// in a fixed order.  Returns the sum in thread 0.
-__device__ __forceinline__ double WorkgroupSum(double v, double* lds4) {
+// Deterministic workgroup sum: xor-butterfly inside each wave, then the
+// waves in a fixed order.  Returns the sum in thread 0.
+__device__ __forceinline__ double WorkgroupSum(double v, double* lds) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  if (lane == 0) lds4[wave] = v;
+  if (lane == 0) lds[wave] = v;
   __syncthreads();
   double t = 0.0;
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int w = 0; w < kBlockThreads / kWave; ++w) t += lds4[w];
+    for (int w = 0; w < kWavesPerBlock; ++w) t += lds[w];
   }
   return t;
 }
 
-// Copy `count` doubles (per-lane staged in LDS, contiguous) to global
-// memory at dst with all 64 lanes cooperating.  16-byte stores when the
-// destination is 16-byte aligned, 8-byte stores otherwise.
+// Copy `count` doubles, staged contiguously in LDS by this wave, to global
+// memory at dst with all 64 lanes: 16-byte stores when dst is 16-byte
+// aligned (1 KiB per wave instruction), 8-byte stores otherwise.
 __device__ __forceinline__ void WaveStore(const double* lds, double* dst, int count, int lane) {
   if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
     const int pairs = count >> 1;
     for (int t = lane; t < pairs; t += kWave) {
       const double2 v = *reinterpret_cast<const double2*>(lds + 2 * t);
-      *reinterpret_cast<double2*>(dst + 2 * t) = v;
+      __builtin_nontemporal_store(v.x, dst + 2 * t);
+      __builtin_nontemporal_store(v.y, dst + 2 * t + 1);
     }
     if ((count & 1) && lane == 0) dst[count - 1] = lds[count - 1];
   } else {
@@ -125,313 +140,448 @@ __device__ __forceinline__ void WaveStore(const double* lds, double* dst, int co
   }
 }
 
-template <class K>
-struct KindTraits {
-  static constexpr int NR = K::kNumResiduals;
-  static constexpr int NB = K::kNumBlocks;
-  static constexpr int S0 = K::kSize0;
-  static constexpr int S1 = K::kSize1;
-  static constexpr int S1p = S1 > 0 ? S1 : 1;
-  static constexpr int N = S0 + S1;
-  static constexpr int D = K::kDataSize;
-  // Doubles of Jacobian a block produces (all slots active, no manifold).
-  static constexpr int kJacPerBlock = NR * N;
-};
-
-// The kernel.  kJac: Jacobian and/or gradient requested (Jets); otherwise
-// the functor runs on plain doubles (the reference always runs Jets,
-// cuda_evaluator_kernel.h:327-345).
-template <class K, int kLoss, bool kJac, bool kAffine>
-__global__ __launch_bounds__(kBlockThreads) void EvaluateGroupKernel(const GroupArgs a) {
+// The functor on plain doubles (kJac = false) or through
+// AutoDifferentiate (include/ceres/internal/autodiff.h:314-381): seed one
+// Jet per parameter with its unit vector, run the functor, split the
+// partials into the row-major per-block Jacobians.
+template <class K, bool kJac>
+CSE_HD bool EvaluateFunctor(const double* d, const double* x0, const double* x1, double* r,
+                            double* J0, double* J1) {
   using Tr = KindTraits<K>;
-  constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
-  constexpr int N = Tr::N, D = Tr::D;
-  // LDS staging for the affine path's stores (per wave: its 64 blocks'
-  // residuals and each slot's Jacobian cells).
-  constexpr int kStage = kAffine ? (kJac ? kWave * NR * N : kWave * NR) : 1;
-  __shared__ double stage[kBlockThreads / kWave][kStage];
-  __shared__ double lds4[kBlockThreads / kWave];
-
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
-  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
-  const bool active = i < a.n;
-  const bool want_res = a.residuals != nullptr;
-  const bool want_jac = kJac && a.jacobian != nullptr;
-  const bool want_grad = kJac && a.gradient != nullptr;
-
-  double cost = 0.0;
-  double r[NR];
-  double J0[NR * S0];
-  double J1[NR * S1p];
-  bool ok = true;
-
-  // --- gather -------------------------------------------------------------
-  int32_t id[2] = {0, 0};
-  const double* p0 = nullptr;
-  const double* p1 = nullptr;
-  int64_t delta[2] = {0, 0};
-  int tan[2] = {S0, S1};
-  bool cst[2] = {false, false};
-  int64_t pjo[2] = {-1, -1};
-  double d[D];
-  if (active) {
-    if constexpr (NB == 2) {
-      const int2 ii = *reinterpret_cast<const int2*>(a.ids + 2 * i);
-      id[0] = ii.x;
-      id[1] = ii.y;
-    } else {
-      id[0] = a.ids[i];
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
+  if constexpr (kJac) {
+    Jet<N> j0[S0], j1[S1p], out[NR];
+#pragma unroll
+    for (int k = 0; k < S0; ++k) j0[k] = Jet<N>(x0[k], k);
+#pragma unroll
+    for (int k = 0; k < S1; ++k) j1[k] = Jet<N>(x1[k], S0 + k);
+    const bool ok = K::Evaluate(d, j0, j1, out);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      r[k] = out[k].a;
+#pragma unroll
+      for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+#pragma unroll
+      for (int c = 0; c < S1; ++c) J1[k * S1p + c] = out[k].v[S0 + c];
     }
+    return ok;
+  } else {
+    return K::Evaluate(d, x0, x1, r);
+  }
+}
+
+// Loss and correction (cuda_evaluator_kernel.h:373-407 /
+// residual_block.cc:159-199).  Returns the block cost.
+template <class K, int kLoss, bool kJac>
+CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, double* J0,
+                             double* J1) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  double sq = 0.0;
 #pragma unroll
-    for (int k = 0; k < D; ++k) d[k] = a.data[i * D + k];
-    if constexpr (kAffine) {
-      p0 = a.state + a.state_base[0] + (int64_t)S0 * id[0];
-      delta[0] = a.delta_base[0] + (int64_t)S0 * id[0];
-      if constexpr (NB == 2) {
-        p1 = a.state + a.state_base[1] + (int64_t)S1 * id[1];
-        delta[1] = a.delta_base[1] + (int64_t)S1 * id[1];
+  for (int k = 0; k < NR; ++k) sq += r[k] * r[k];
+  const bool robust = (kLoss != kLossTrivial || lp.scaled) && apply_loss;
+  if (!robust) return 0.5 * sq;
+  double rho[3];
+  EvaluateLoss<kLoss>(lp, sq, rho);
+  const Corrector corr(sq, rho);
+  if constexpr (kJac) {
+    corr.template CorrectJacobian<NR, S0>(r, J0);
+    if constexpr (S1 > 0) corr.template CorrectJacobian<NR, S1p>(r, J1);
+  }
+  corr.template CorrectResiduals<NR>(r);
+  return 0.5 * rho[0];
+}
+
+// Stage one wave's outputs in LDS and write each contiguous segment.  The
+// wave's blocks [i0, i0 + nw) are contiguous in every segment:
+//   residuals: [res_base + kR*i0, + kR*nw)
+//   kCrs = false (BlockSparseMatrix): slot j's packed cells at
+//       [jac_base[j][0] + stride_j*i0, + kR*size_j*nw)
+//   kCrs = true (CompressedRowSparseMatrix): whole blocks, kR rows of N
+//       columns, at [row0 + kR*N*i0, + kR*N*nw)
+template <class K, bool kJac, bool kCrs>
+__device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
+                                              int64_t i0, int nw, const double* r,
+                                              const double* J0, const double* J1) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
+  if (nw <= 0) return;
+  if (a.residuals) {
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    WaveStore(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (kJac) {
+    if (!a.jacobian) return;
+    if constexpr (kCrs) {
+      const int64_t row0 = a.jac_base[0][0] < a.jac_base[NB - 1][0] ? a.jac_base[0][0]
+                                                                      : a.jac_base[NB - 1][0];
+      if (active) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          const int c0 = (int)(a.jac_base[0][k] - row0);
+#pragma unroll
+          for (int c = 0; c < S0; ++c) st[lane * NR * N + c0 + c] = J0[k * S0 + c];
+          if constexpr (S1 > 0) {
+            const int c1 = (int)(a.jac_base[1][k] - row0);
+#pragma unroll
+            for (int c = 0; c < S1; ++c) st[lane * NR * N + c1 + c] = J1[k * S1p + c];
+          }
+        }
       }
+      __builtin_amdgcn_wave_barrier();
+      WaveStore(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N, lane);
+      __builtin_amdgcn_wave_barrier();
     } else {
+      if (active) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const PbDev pb = a.pbs[id[j]];
-        const double* p = (pb.is_constant ? a.cstate : a.state) + pb.state_offset;
-        if (j == 0) p0 = p; else p1 = p;
-        delta[j] = pb.delta_offset;
-        tan[j] = pb.tangent_size;
-        cst[j] = pb.is_constant != 0;
-        pjo[j] = pb.plus_jacobian_offset;
+        for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
+      }
+      __builtin_amdgcn_wave_barrier();
+      WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
+      __builtin_amdgcn_wave_barrier();
+      if constexpr (S1 > 0) {
+        if (active) {
+#pragma unroll
+          for (int q = 0; q < NR * S1; ++q) st[lane * NR * S1 + q] = J1[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        WaveStore(st, a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0, nw * NR * S1, lane);
+        __builtin_amdgcn_wave_barrier();
       }
     }
   }
+}
 
-  if (active) {
-    double x0[S0], x1[S1p];
+// Gradient g += J^T r with device-scope FP64 atomics (native
+// global_atomic_add_f64), as cuda_evaluator_kernel.h:149-160.
+template <class K>
+__device__ __forceinline__ void AddGradient(double* g0, double* g1, int t0, int t1,
+                                            const double* r, const double* J0,
+                                            const double* J1) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  if (g0) {
 #pragma unroll
-    for (int k = 0; k < S0; ++k) x0[k] = p0[k];
+    for (int c = 0; c < S0; ++c) {
+      if (c >= t0) break;
+      double s = 0.0;
 #pragma unroll
-    for (int k = 0; k < S1; ++k) x1[k] = p1[k];
-
-    // --- autodiff -----------------------------------------------------------
-    if constexpr (kJac) {
-      // AutoDifferentiate (include/ceres/internal/autodiff.h:314-381).
-      Jet<N> j0[S0], j1[S1p], out[NR];
-#pragma unroll
-      for (int k = 0; k < S0; ++k) j0[k] = Jet<N>(x0[k], k);
-#pragma unroll
-      for (int k = 0; k < S1; ++k) j1[k] = Jet<N>(x1[k], S0 + k);
-      ok = K::Evaluate(d, j0, j1, out);
-#pragma unroll
-      for (int k = 0; k < NR; ++k) {
-        r[k] = out[k].a;
-#pragma unroll
-        for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
-#pragma unroll
-        for (int c = 0; c < S1; ++c) J1[k * S1p + c] = out[k].v[S0 + c];
-      }
-    } else {
-      ok = K::Evaluate(d, x0, x1, r);
+      for (int k = 0; k < NR; ++k) s += J0[k * S0 + c] * r[k];
+      unsafeAtomicAdd(g0 + c, s);
     }
+  }
+  if (g1) {
+#pragma unroll
+    for (int c = 0; c < S1; ++c) {
+      if (c >= t1) break;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < NR; ++k) s += J1[k * S1p + c] * r[k];
+      unsafeAtomicAdd(g1 + c, s);
+    }
+  }
+}
+
+// Inputs of one block (affine path).
+template <class K>
+struct AffineInputs {
+  double d[KindTraits<K>::D];
+  double x0[KindTraits<K>::S0];
+  double x1[KindTraits<K>::S1p];
+  int32_t id0, id1;
+};
+
+template <class K>
+__device__ __forceinline__ int2 LoadIds(const GroupArgs& a, int64_t i) {
+  if constexpr (KindTraits<K>::NB == 2) {
+    return *reinterpret_cast<const int2*>(a.ids + 2 * i);
+  } else {
+    return make_int2(a.ids[i], 0);
+  }
+}
+
+template <class K>
+__device__ __forceinline__ void Gather(const GroupArgs& a, int64_t i, int2 id, AffineInputs<K>* in) {
+  using Tr = KindTraits<K>;
+  constexpr int S0 = Tr::S0, S1 = Tr::S1, D = Tr::D;
+  if constexpr (D == 2) {
+    const double2 v = *reinterpret_cast<const double2*>(a.data + 2 * i);
+    in->d[0] = v.x;
+    in->d[1] = v.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) in->d[k] = a.data[i * D + k];
+  }
+  const double* p0 = a.state + a.state_base[0] + (int64_t)S0 * id.x;
+#pragma unroll
+  for (int k = 0; k < S0; ++k) in->x0[k] = p0[k];
+  if constexpr (S1 > 0) {
+    const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < S1; ++k) in->x1[k] = p1[k];
+  }
+  in->id0 = id.x;
+  in->id1 = id.y;
+}
+
+// Per-lane (unstaged) stores of one block: the wave's stores of a segment
+// then cover it with 8/16-byte pieces at the block stride.
+template <class K, bool kJac, bool kCrs>
+__device__ __forceinline__ void DirectStore(const GroupArgs& a, int64_t i, const double* r,
+                                            const double* J0, const double* J1) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  if (a.residuals) {
+    double* dst = a.residuals + a.res_base + (int64_t)NR * i;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) dst[k] = r[k];
+  }
+  if constexpr (kJac) {
+    if (!a.jacobian) return;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      double* d0 = a.jacobian + a.jac_base[0][k] + a.jac_stride[0] * i;
+#pragma unroll
+      for (int c = 0; c < S0; ++c) d0[c] = J0[k * S0 + c];
+      if constexpr (S1 > 0) {
+        double* d1 = a.jacobian + a.jac_base[1][k] + a.jac_stride[1] * i;
+#pragma unroll
+        for (int c = 0; c < S1; ++c) d1[c] = J1[k * S1p + c];
+      }
+    }
+  }
+}
+
+// The hot path: persistent, software-pipelined, table-free.
+//   kPrefetch 2: gathers of chunk c+1 and ids of chunk c+2 in flight while
+//                chunk c computes; 1: only the ids of chunk c+1; 0: none;
+//                -1: not persistent (one chunk per wave, grid = all chunks).
+//   kStage: LDS-staged 1 KiB-per-instruction stores vs per-lane stores.
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage>
+__device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
+  constexpr int kStageLane =
+      !kStage ? 1 : kJac ? (kCrs ? NR * N : (NR * S0 > NR * S1 ? NR * S0 : NR * S1)) : NR;
+  __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
+  __shared__ double lds_sum[kWavesPerBlock];
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int64_t num_chunks = (a.n + kWave - 1) / kWave;
+  const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock;
+  int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const bool want_grad = kJac && a.gradient != nullptr;
+  double* st = stage[wave];
+  double cost_acc = 0.0;
+  bool all_ok = true;
+
+  auto idx = [&](int64_t chunk) {
+    const int64_t i = chunk * kWave + lane;
+    return i < a.n ? i : a.n - 1;  // inactive lanes re-read the last block
+  };
+  AffineInputs<K> cur;
+  int2 ids_next = make_int2(0, 0);
+  if constexpr (kPrefetch == 2) {
+    if (c < num_chunks) Gather<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur);
+    if (c + stride < num_chunks) ids_next = LoadIds<K>(a, idx(c + stride));
+  } else if constexpr (kPrefetch == 1) {
+    if (c < num_chunks) ids_next = LoadIds<K>(a, idx(c));
+  }
+
+  for (; c < num_chunks; c += (kPrefetch < 0 ? num_chunks : stride)) {
+    const int64_t cn = c + stride;
+    AffineInputs<K> nxt;
+    if constexpr (kPrefetch == 2) {
+      if (cn < num_chunks) Gather<K>(a, idx(cn), ids_next, &nxt);
+      if (cn + stride < num_chunks) ids_next = LoadIds<K>(a, idx(cn + stride));
+    } else if constexpr (kPrefetch == 1) {
+      Gather<K>(a, idx(c), ids_next, &cur);
+      if (cn < num_chunks) ids_next = LoadIds<K>(a, idx(cn));
+    } else {
+      Gather<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur);
+    }
+    (void)cn;
+
+    const int64_t i0 = c * kWave;
+    const int64_t rem = a.n - i0;
+    const int nw = rem < kWave ? (int)rem : kWave;
+    const bool active = lane < nw;
+    double r[NR], J0[NR * S0], J1[NR * S1p];
+    bool ok = EvaluateFunctor<K, kJac>(cur.d, cur.x0, cur.x1, r, J0, J1);
     if (ok && a.check_finite) {
       bool bad = AnyNonFinite<NR>(r);
       if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
       ok = !bad;
     }
-    if (!ok) *a.status = 1;
-
-    double sq = 0.0;
-#pragma unroll
-    for (int k = 0; k < NR; ++k) sq += r[k] * r[k];
-
-    if constexpr (kJac && !kAffine) {
-      // Local Jacobian = ambient Jacobian * PlusJacobian
-      // (cuda_evaluator_kernel.h:355-371; residual_block.cc:133-156).
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        if (pjo[j] < 0) continue;
-        const double* PJ = a.plus_jacobians + pjo[j];
-        const int t = tan[j];
-        constexpr int kS = 0;
-        (void)kS;
-        if (j == 0) {
-          double L[NR * S0];
-#pragma unroll
-          for (int k = 0; k < NR; ++k)
-#pragma unroll
-            for (int c = 0; c < S0; ++c) {
-              double s = 0.0;
-              if (c < t) {
-#pragma unroll
-                for (int m = 0; m < S0; ++m) s += J0[k * S0 + m] * PJ[m * t + c];
-              }
-              L[k * S0 + c] = s;
-            }
-#pragma unroll
-          for (int q = 0; q < NR * S0; ++q) J0[q] = L[q];
-        } else {
-          double L[NR * S1p];
-#pragma unroll
-          for (int k = 0; k < NR; ++k)
-#pragma unroll
-            for (int c = 0; c < S1; ++c) {
-              double s = 0.0;
-              if (c < t) {
-#pragma unroll
-                for (int m = 0; m < S1; ++m) s += J1[k * S1p + m] * PJ[m * t + c];
-              }
-              L[k * S1p + c] = s;
-            }
-#pragma unroll
-          for (int q = 0; q < NR * S1p; ++q) J1[q] = L[q];
-        }
-      }
+    const double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+    if (active) {
+      all_ok = all_ok && ok;
+      cost_acc += cost;
+      if (want_grad)
+        AddGradient<K>(a.gradient + a.delta_base[0] + (int64_t)S0 * cur.id0,
+                       S1 > 0 ? a.gradient + a.delta_base[1] + (int64_t)S1 * cur.id1 : nullptr,
+                       S0, S1, r, J0, J1);
     }
-
-    // --- loss and correction (cuda_evaluator_kernel.h:373-407) -------------
-    const bool robust = (kLoss != kLossTrivial || a.loss.scaled) && a.apply_loss;
-    if (!robust) {
-      cost = 0.5 * sq;
-    } else {
-      double rho[3];
-      EvaluateLoss<kLoss>(a.loss, sq, rho);
-      cost = 0.5 * rho[0];
-      const Corrector corr(sq, rho);
-      if constexpr (kJac) {
-        corr.template CorrectJacobian<NR, S0>(r, J0);
-        if constexpr (S1 > 0) corr.template CorrectJacobian<NR, S1p>(r, J1);
-      }
-      corr.template CorrectResiduals<NR>(r);
+    if constexpr (kStage) {
+      StageAndStore<K, kJac, kCrs>(a, st, lane, active, i0, nw, r, J0, J1);
+    } else if (active) {
+      DirectStore<K, kJac, kCrs>(a, i0 + lane, r, J0, J1);
     }
-    if (!ok) cost = 0.0;
-
-    // --- gradient g += J^T r (cuda_evaluator_kernel.h:149-160,409-414) ------
-    if (want_grad && ok) {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        if (cst[j]) continue;
-        double* g = a.gradient + delta[j];
-        if (j == 0) {
-#pragma unroll
-          for (int c = 0; c < S0; ++c) {
-            if (c >= tan[0]) break;
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k < NR; ++k) s += J0[k * S0 + c] * r[k];
-            unsafeAtomicAdd(g + c, s);
-          }
-        } else {
-#pragma unroll
-          for (int c = 0; c < S1; ++c) {
-            if (c >= tan[1]) break;
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k < NR; ++k) s += J1[k * S1p + c] * r[k];
-            unsafeAtomicAdd(g + c, s);
-          }
-        }
-      }
-    }
+    if constexpr (kPrefetch == 2) cur = nxt;
   }
+  if (!all_ok) *a.status = 1;
+  const double t = WorkgroupSum(cost_acc, lds_sum);
+  if (threadIdx.x == 0) a.partials[blockIdx.x] = t;
+}
 
-  // --- stores --------------------------------------------------------------
-  if constexpr (kAffine) {
-    // Stage this wave's outputs in LDS, then write each contiguous segment
-    // with all lanes.  Wave-uniform: every lane takes the same path, the
-    // wave's block range [i0, i0 + nw) is contiguous in every segment.
-    const int64_t i0 = (int64_t)blockIdx.x * kBlockThreads + wave * kWave;
-    const int64_t rem = a.n - i0;
-    const int nw = rem <= 0 ? 0 : (rem < kWave ? (int)rem : kWave);
-    double* st = stage[wave];
-    if (want_res && nw > 0) {
-      if (active) {
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kMinWaves>
+__global__ __launch_bounds__(kBlockThreads, kMinWaves) void EvaluateAffinePersistent(
+    const GroupArgs a) {
+  AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage>(a);
+}
+
+// Same kernel without an occupancy request (the compiler's default target).
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage>
+__global__ __launch_bounds__(kBlockThreads) void EvaluateAffinePersistentD(const GroupArgs a) {
+  AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage>(a);
+}
+
+// The general (table) path; also runs affine groups when
+// force_general_layout is set.  One block per lane, one launch-wide grid.
+template <class K, int kLoss, bool kJac>
+__global__ __launch_bounds__(kBlockThreads) void EvaluateGroupKernel(const GroupArgs a) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  __shared__ double lds_sum[kWavesPerBlock];
+
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  const bool active = i < a.n;
+  const bool want_jac = kJac && a.jacobian != nullptr;
+  const bool want_grad = kJac && a.gradient != nullptr;
+  double cost = 0.0;
+
+  if (active) {
+    int32_t id[2] = {0, 0};
+    const int2 ii = LoadIds<K>(a, i);
+    id[0] = ii.x;
+    id[1] = ii.y;
+    double d[Tr::D];
 #pragma unroll
-        for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
-      }
-      __builtin_amdgcn_wave_barrier();
-      WaveStore(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
-      __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < Tr::D; ++k) d[k] = a.data[i * Tr::D + k];
+    const double* p[2] = {nullptr, nullptr};
+    int64_t delta[2] = {0, 0};
+    int tan[2] = {S0, S1};
+    bool cst[2] = {false, false};
+    int64_t pjo[2] = {-1, -1};
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const PbDev pb = a.pbs[id[j]];
+      p[j] = (pb.is_constant ? a.cstate : a.state) + pb.state_offset;
+      delta[j] = pb.delta_offset;
+      tan[j] = pb.tangent_size;
+      cst[j] = pb.is_constant != 0;
+      pjo[j] = pb.plus_jacobian_offset;
+    }
+    double x0[S0], x1[S1p];
+#pragma unroll
+    for (int k = 0; k < S0; ++k) x0[k] = p[0][k];
+#pragma unroll
+    for (int k = 0; k < S1; ++k) x1[k] = p[1][k];
+
+    double r[NR], J0[NR * S0], J1[NR * S1p];
+    bool ok = EvaluateFunctor<K, kJac>(d, x0, x1, r, J0, J1);
+    if (ok && a.check_finite) {
+      bool bad = AnyNonFinite<NR>(r);
+      if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
+      ok = !bad;
     }
     if constexpr (kJac) {
-      if (want_jac && nw > 0) {
-        // Slot j occupies rows k at jac_base[j][k] + jac_stride[j]*i.  Two
-        // shapes are contiguous per wave: a packed cell (rows adjacent,
-        // stride = kR*size; BlockSparseMatrix) and interleaved rows
-        // covering all slots (stride = kR*N; CompressedRowSparseMatrix).
-        const bool crs = a.jac_stride[0] == (int64_t)NR * N;
-        if (crs) {
-          // Row k of block i = [slot in column order] at jac_base[.][k].
-          // Build the block's kR*N doubles in memory order.
-          const int64_t row0 = a.jac_base[0][0] < a.jac_base[NB - 1][0] ? a.jac_base[0][0]
-                                                                          : a.jac_base[NB - 1][0];
-          if (active) {
+      // Local Jacobian = ambient Jacobian * PlusJacobian
+      // (cuda_evaluator_kernel.h:355-371; residual_block.cc:133-156).
+      if (pjo[0] >= 0) {
+        const double* PJ = a.plus_jacobians + pjo[0];
+        const int t = tan[0];
+        double L[NR * S0];
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
+        for (int k = 0; k < NR; ++k)
 #pragma unroll
-              for (int c = 0; c < S0; ++c)
-                st[lane * NR * N + (int)(a.jac_base[0][k] - row0) + c] = J0[k * S0 + c];
+          for (int c = 0; c < S0; ++c) {
+            double s = 0.0;
+            if (c < t) {
 #pragma unroll
-              for (int c = 0; c < S1; ++c)
-                st[lane * NR * N + (int)(a.jac_base[1][k] - row0) + c] = J1[k * S1p + c];
+              for (int m = 0; m < S0; ++m) s += J0[k * S0 + m] * PJ[m * t + c];
             }
+            L[k * S0 + c] = s;
           }
-          __builtin_amdgcn_wave_barrier();
-          WaveStore(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N, lane);
-          __builtin_amdgcn_wave_barrier();
-        } else {
-          if (active) {
 #pragma unroll
-            for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
-          }
-          __builtin_amdgcn_wave_barrier();
-          WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
-          __builtin_amdgcn_wave_barrier();
-          if constexpr (S1 > 0) {
-            if (active) {
+        for (int q = 0; q < NR * S0; ++q) J0[q] = L[q];
+      }
+      if (S1 > 0 && pjo[1] >= 0) {
+        const double* PJ = a.plus_jacobians + pjo[1];
+        const int t = tan[1];
+        double L[NR * S1p];
 #pragma unroll
-              for (int q = 0; q < NR * S1; ++q) st[lane * NR * S1 + q] = J1[q];
+        for (int k = 0; k < NR; ++k)
+#pragma unroll
+          for (int c = 0; c < S1; ++c) {
+            double s = 0.0;
+            if (c < t) {
+#pragma unroll
+              for (int m = 0; m < S1; ++m) s += J1[k * S1p + m] * PJ[m * t + c];
             }
-            __builtin_amdgcn_wave_barrier();
-            WaveStore(st, a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0, nw * NR * S1,
-                      lane);
-            __builtin_amdgcn_wave_barrier();
+            L[k * S1p + c] = s;
           }
-        }
+#pragma unroll
+        for (int q = 0; q < NR * S1p; ++q) J1[q] = L[q];
       }
     }
-  } else if (active && ok) {
-    const int64_t gi = GlobalIndex(a, i);
-    if (want_res) {
-      double* dst = a.residuals + a.residual_layout[gi];
+    cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+    if (!ok) {
+      cost = 0.0;
+      *a.status = 1;
+    } else {
+      if (want_grad)
+        AddGradient<K>(cst[0] ? nullptr : a.gradient + delta[0],
+                       (S1 > 0 && !cst[1]) ? a.gradient + delta[1] : nullptr, tan[0], tan[1], r,
+                       J0, J1);
+      const int64_t gi = a.gindex ? a.gindex[i] : a.first + i;
+      if (a.residuals) {
+        double* dst = a.residuals + a.residual_layout[gi];
 #pragma unroll
-      for (int k = 0; k < NR; ++k) dst[k] = r[k];
-    }
-    if (want_jac) {
-      // WriteJacobians (cuda_evaluator_kernel.h:260-294): row k of the
-      // a-th active slot goes to values + offsets[layout[gi] + a*kR + k].
-      int64_t idx = a.jac_layout[gi];
+        for (int k = 0; k < NR; ++k) dst[k] = r[k];
+      }
+      if (want_jac) {
+        // WriteJacobians (cuda_evaluator_kernel.h:260-294): row k of the
+        // a-th active slot goes to values + offsets[layout[gi] + a*kR + k].
+        int64_t q = a.jac_layout[gi];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        if (cst[j]) continue;
+        for (int j = 0; j < NB; ++j) {
+          if (cst[j]) continue;
 #pragma unroll
-        for (int k = 0; k < NR; ++k) {
-          double* dst = a.jacobian + a.jac_offsets[idx++];
-          if (j == 0) {
+          for (int k = 0; k < NR; ++k) {
+            double* dst = a.jacobian + a.jac_offsets[q++];
+            if (j == 0) {
 #pragma unroll
-            for (int c = 0; c < S0; ++c)
-              if (c < tan[0]) dst[c] = J0[k * S0 + c];
-          } else {
+              for (int c = 0; c < S0; ++c)
+                if (c < tan[0]) dst[c] = J0[k * S0 + c];
+            } else {
 #pragma unroll
-            for (int c = 0; c < S1; ++c)
-              if (c < tan[1]) dst[c] = J1[k * S1p + c];
+              for (int c = 0; c < S1; ++c)
+                if (c < tan[1]) dst[c] = J1[k * S1p + c];
+            }
           }
         }
       }
     }
   }
-
-  // --- cost partial --------------------------------------------------------
-  const double t = WorkgroupSum(cost, lds4);
+  const double t = WorkgroupSum(cost, lds_sum);
   if (threadIdx.x == 0) a.partials[blockIdx.x] = t;
 }
 
