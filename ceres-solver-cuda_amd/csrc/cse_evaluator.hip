@@ -104,10 +104,10 @@ void LaunchGeneral(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
-template <class K, int L, bool J, bool Crs, int Pf = 2, bool St = true, int Mw = 0>
+template <class K, int L, bool J, bool Crs, int Pf = 2, bool St = true, int Mw = 0, int Dbg = 0>
 void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (Mw == 0) {
-    hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St>),
+    hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St, Dbg>),
                        dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
   } else {
     hipLaunchKernelGGL((cse::EvaluateAffinePersistent<K, L, J, Crs, Pf, St, Mw>),
@@ -131,6 +131,11 @@ LaunchFn SnavelyVariant(int v) {
     case 7: return &LaunchAffine<K, L, true, false, 1, true, 4>;
     case 8: return &LaunchAffine<K, L, true, false, -1, true, 0>;
     case 9: return &LaunchAffine<K, L, true, false, -1, false, 0>;
+    // Diagnostics (wrong results by design): memory floor, compute floor,
+    // plain (not non-temporal) stores.
+    case 10: return &LaunchAffine<K, L, true, false, -1, true, 0, 1>;
+    case 11: return &LaunchAffine<K, L, true, false, -1, true, 0, 2>;
+    case 12: return &LaunchAffine<K, L, true, false, -1, true, 0, 3>;
     default: return nullptr;
   }
 }

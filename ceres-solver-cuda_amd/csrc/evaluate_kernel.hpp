@@ -126,13 +126,18 @@ __device__ __forceinline__ double WorkgroupSum(double v, double* lds) {
 // Copy `count` doubles, staged contiguously in LDS by this wave, to global
 // memory at dst with all 64 lanes: 16-byte stores when dst is 16-byte
 // aligned (1 KiB per wave instruction), 8-byte stores otherwise.
+template <bool kNt = true>
 __device__ __forceinline__ void WaveStore(const double* lds, double* dst, int count, int lane) {
   if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
     const int pairs = count >> 1;
     for (int t = lane; t < pairs; t += kWave) {
       const double2 v = *reinterpret_cast<const double2*>(lds + 2 * t);
-      __builtin_nontemporal_store(v.x, dst + 2 * t);
-      __builtin_nontemporal_store(v.y, dst + 2 * t + 1);
+      if constexpr (kNt) {
+        __builtin_nontemporal_store(v.x, dst + 2 * t);
+        __builtin_nontemporal_store(v.y, dst + 2 * t + 1);
+      } else {
+        *reinterpret_cast<double2*>(dst + 2 * t) = v;
+      }
     }
     if ((count & 1) && lane == 0) dst[count - 1] = lds[count - 1];
   } else {
@@ -200,7 +205,7 @@ CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, d
 //       [jac_base[j][0] + stride_j*i0, + kR*size_j*nw)
 //   kCrs = true (CompressedRowSparseMatrix): whole blocks, kR rows of N
 //       columns, at [row0 + kR*N*i0, + kR*N*nw)
-template <class K, bool kJac, bool kCrs>
+template <class K, bool kJac, bool kCrs, bool kNt = true>
 __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
                                               int64_t i0, int nw, const double* r,
                                               const double* J0, const double* J1) {
@@ -213,7 +218,7 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
       for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
     }
     __builtin_amdgcn_wave_barrier();
-    WaveStore(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
+    WaveStore<kNt>(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
     __builtin_amdgcn_wave_barrier();
   }
   if constexpr (kJac) {
@@ -235,7 +240,7 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
         }
       }
       __builtin_amdgcn_wave_barrier();
-      WaveStore(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N, lane);
+      WaveStore<kNt>(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N, lane);
       __builtin_amdgcn_wave_barrier();
     } else {
       if (active) {
@@ -243,7 +248,7 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
         for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
       }
       __builtin_amdgcn_wave_barrier();
-      WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
+      WaveStore<kNt>(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
       __builtin_amdgcn_wave_barrier();
       if constexpr (S1 > 0) {
         if (active) {
@@ -363,7 +368,10 @@ __device__ __forceinline__ void DirectStore(const GroupArgs& a, int64_t i, const
 //                chunk c computes; 1: only the ids of chunk c+1; 0: none;
 //                -1: not persistent (one chunk per wave, grid = all chunks).
 //   kStage: LDS-staged 1 KiB-per-instruction stores vs per-lane stores.
-template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage>
+//   kDebug (diagnostic builds only): 1 replaces the functor with a trivial
+//   map of its inputs (memory-path floor), 2 skips the stores (compute
+//   floor), 3 stores without the non-temporal hint.
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0>
 __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
@@ -414,13 +422,31 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
     const int nw = rem < kWave ? (int)rem : kWave;
     const bool active = lane < nw;
     double r[NR], J0[NR * S0], J1[NR * S1p];
-    bool ok = EvaluateFunctor<K, kJac>(cur.d, cur.x0, cur.x1, r, J0, J1);
+    bool ok = true;
+    if constexpr (kDebug == 1) {
+#pragma unroll
+      for (int k = 0; k < NR; ++k) r[k] = cur.d[k % Tr::D] - cur.x1[k % S1p];
+#pragma unroll
+      for (int q = 0; q < NR * S0; ++q) J0[q] = cur.x0[q % S0] * cur.d[0];
+#pragma unroll
+      for (int q = 0; q < NR * S1p; ++q) J1[q] = cur.x1[q % S1p] * cur.d[1 % Tr::D];
+    } else {
+      ok = EvaluateFunctor<K, kJac>(cur.d, cur.x0, cur.x1, r, J0, J1);
+    }
     if (ok && a.check_finite) {
       bool bad = AnyNonFinite<NR>(r);
       if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
       ok = !bad;
     }
-    const double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+    double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+    if constexpr (kDebug == 2) {
+#pragma unroll
+      for (int q = 0; q < NR * S0; ++q) cost += J0[q];
+#pragma unroll
+      for (int q = 0; q < NR * S1p; ++q) cost += J1[q];
+#pragma unroll
+      for (int k = 0; k < NR; ++k) cost += r[k];
+    }
     if (active) {
       all_ok = all_ok && ok;
       cost_acc += cost;
@@ -429,8 +455,9 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
                        S1 > 0 ? a.gradient + a.delta_base[1] + (int64_t)S1 * cur.id1 : nullptr,
                        S0, S1, r, J0, J1);
     }
-    if constexpr (kStage) {
-      StageAndStore<K, kJac, kCrs>(a, st, lane, active, i0, nw, r, J0, J1);
+    if constexpr (kDebug == 2) {
+    } else if constexpr (kStage) {
+      StageAndStore<K, kJac, kCrs, kDebug != 3>(a, st, lane, active, i0, nw, r, J0, J1);
     } else if (active) {
       DirectStore<K, kJac, kCrs>(a, i0 + lane, r, J0, J1);
     }
@@ -448,9 +475,9 @@ __global__ __launch_bounds__(kBlockThreads, kMinWaves) void EvaluateAffinePersis
 }
 
 // Same kernel without an occupancy request (the compiler's default target).
-template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage>
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0>
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffinePersistentD(const GroupArgs a) {
-  AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage>(a);
+  AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage, kDebug>(a);
 }
 
 // The general (table) path; also runs affine groups when
