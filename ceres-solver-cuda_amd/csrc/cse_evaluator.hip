@@ -104,10 +104,11 @@ void LaunchGeneral(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
-template <class K, int L, bool J, bool Crs, int Pf = 2, bool St = true, int Mw = 0, int Dbg = 0>
+template <class K, int L, bool J, bool Crs, int Pf = 2, bool St = true, int Mw = 0, int Dbg = 0,
+          bool Co = false>
 void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (Mw == 0) {
-    hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St, Dbg>),
+    hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St, Dbg, Co>),
                        dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
   } else {
     hipLaunchKernelGGL((cse::EvaluateAffinePersistent<K, L, J, Crs, Pf, St, Mw>),
@@ -136,6 +137,9 @@ LaunchFn SnavelyVariant(int v) {
     case 10: return &LaunchAffine<K, L, true, false, -1, true, 0, 1>;
     case 11: return &LaunchAffine<K, L, true, false, -1, true, 0, 2>;
     case 12: return &LaunchAffine<K, L, true, false, -1, true, 0, 3>;
+    case 13: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, true>;
+    case 14: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, true>;
+    case 15: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, true>;
     default: return nullptr;
   }
 }
@@ -195,7 +199,8 @@ int PersistentWgPerCu(const KindShape& k, int policy) {
     if (v > 0) return v;
     if (v == 0) return 1 << 20;  // one chunk per wave: not persistent
   }
-  if (AffineVariant() >= 8) return 1 << 20;  // the non-persistent variants
+  const int v = AffineVariant();
+  if (v >= 8 && v != 15) return 1 << 20;  // the non-persistent variants
   const int lane_doubles = policy == kAffineCrs ? k.nr * (k.s0 + k.s1)
                                                 : k.nr * std::max(k.s0, k.s1);
   const int lds = cse::kWavesPerBlock * cse::kWave * lane_doubles * 8 + 64;

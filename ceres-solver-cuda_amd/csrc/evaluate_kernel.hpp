@@ -363,6 +363,50 @@ __device__ __forceinline__ void DirectStore(const GroupArgs& a, int64_t i, const
   }
 }
 
+// Gather with slot 0 (the camera) loaded wave-cooperatively: the wave's 64
+// parameter blocks are fetched as 64*S0 consecutive 8-byte pieces, piece p
+// by lane p % 64 of load p / 64, so each load instruction walks the bytes of
+// a few whole blocks (~8 cache lines) instead of 64 scattered lines, then
+// the pieces are redistributed through LDS (lds: 64*S0 doubles of this
+// wave).  Slot 1 (the point) and the functor data are per-lane loads: in
+// Schur order consecutive blocks share points, so those already coalesce.
+template <class K>
+__device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 id,
+                                           AffineInputs<K>* in, double* lds, int lane) {
+  using Tr = KindTraits<K>;
+  constexpr int S0 = Tr::S0, S1 = Tr::S1, D = Tr::D;
+  if constexpr (D == 2) {
+    const double2 v = *reinterpret_cast<const double2*>(a.data + 2 * i);
+    in->d[0] = v.x;
+    in->d[1] = v.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) in->d[k] = a.data[i * D + k];
+  }
+  if constexpr (S1 > 0) {
+    const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < S1; ++k) in->x1[k] = p1[k];
+  }
+  const double* base0 = a.state + a.state_base[0];
+  double piece[S0];
+#pragma unroll
+  for (int k = 0; k < S0; ++k) {
+    const int p = k * kWave + lane;
+    const int t = p / S0, q = p - t * S0;
+    const int cid = __shfl(id.x, t, kWave);
+    piece[k] = base0[(int64_t)S0 * cid + q];
+  }
+#pragma unroll
+  for (int k = 0; k < S0; ++k) lds[k * kWave + lane] = piece[k];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0 + k];
+  __builtin_amdgcn_wave_barrier();
+  in->id0 = id.x;
+  in->id1 = id.y;
+}
+
 // The hot path: persistent, software-pipelined, table-free.
 //   kPrefetch 2: gathers of chunk c+1 and ids of chunk c+2 in flight while
 //                chunk c computes; 1: only the ids of chunk c+1; 0: none;
@@ -371,12 +415,16 @@ __device__ __forceinline__ void DirectStore(const GroupArgs& a, int64_t i, const
 //   kDebug (diagnostic builds only): 1 replaces the functor with a trivial
 //   map of its inputs (memory-path floor), 2 skips the stores (compute
 //   floor), 3 stores without the non-temporal hint.
-template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0>
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0,
+          bool kCoop = false>
 __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
-  constexpr int kStageLane =
+  constexpr int kOutLane =
       !kStage ? 1 : kJac ? (kCrs ? NR * N : (NR * S0 > NR * S1 ? NR * S0 : NR * S1)) : NR;
+  // The staging buffer also holds the cooperative camera gather (used
+  // before the outputs are staged).
+  constexpr int kStageLane = kCoop && S0 > kOutLane ? S0 : kOutLane;
   __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
   __shared__ double lds_sum[kWavesPerBlock];
 
@@ -412,6 +460,8 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
     } else if constexpr (kPrefetch == 1) {
       Gather<K>(a, idx(c), ids_next, &cur);
       if (cn < num_chunks) ids_next = LoadIds<K>(a, idx(cn));
+    } else if constexpr (kCoop) {
+      GatherCoop<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur, st, lane);
     } else {
       Gather<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur);
     }
@@ -475,9 +525,10 @@ __global__ __launch_bounds__(kBlockThreads, kMinWaves) void EvaluateAffinePersis
 }
 
 // Same kernel without an occupancy request (the compiler's default target).
-template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0>
+template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0,
+          bool kCoop = false>
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffinePersistentD(const GroupArgs a) {
-  AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage, kDebug>(a);
+  AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage, kDebug, kCoop>(a);
 }
 
 // The general (table) path; also runs affine groups when
