@@ -145,6 +145,44 @@ __device__ __forceinline__ void WaveStore(const double* lds, double* dst, int co
   }
 }
 
+// WaveStore for a full 64-block chunk: kCount (compile time) doubles, all
+// LDS reads issued before any global store so the wave waits for LDS once
+// per segment instead of once per 1 KiB piece.  dst is 16-byte aligned.
+template <int kCount, bool kNt = true>
+__device__ __forceinline__ void WaveStoreFull(const double* lds, double* dst, int lane) {
+  constexpr int kPairs = kCount / 2;
+  constexpr int kIters = (kPairs + kWave - 1) / kWave;
+  double2 v[kIters];
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int t = it * kWave + lane;
+    if (kPairs % kWave == 0 || t < kPairs) v[it] = reinterpret_cast<const double2*>(lds)[t];
+  }
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int t = it * kWave + lane;
+    if (kPairs % kWave == 0 || t < kPairs) {
+      if constexpr (kNt) {
+        __builtin_nontemporal_store(v[it].x, dst + 2 * t);
+        __builtin_nontemporal_store(v[it].y, dst + 2 * t + 1);
+      } else {
+        reinterpret_cast<double2*>(dst)[t] = v[it];
+      }
+    }
+  }
+  if constexpr (kCount % 2 != 0) {
+    if (lane == 0) dst[kCount - 1] = lds[kCount - 1];
+  }
+}
+
+template <int kCount, bool kNt>
+__device__ __forceinline__ void WaveStoreAny(const double* lds, double* dst, int count, int lane) {
+  if (count == kCount && (reinterpret_cast<uintptr_t>(dst) & 15) == 0)
+    WaveStoreFull<kCount, kNt>(lds, dst, lane);
+  else
+    WaveStore<kNt>(lds, dst, count, lane);
+}
+
 // The functor on plain doubles (kJac = false) or through
 // AutoDifferentiate (include/ceres/internal/autodiff.h:314-381): seed one
 // Jet per parameter with its unit vector, run the functor, split the
@@ -218,7 +256,7 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
       for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
     }
     __builtin_amdgcn_wave_barrier();
-    WaveStore<kNt>(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
+    WaveStoreAny<kWave * NR, kNt>(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
     __builtin_amdgcn_wave_barrier();
   }
   if constexpr (kJac) {
@@ -240,7 +278,8 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
         }
       }
       __builtin_amdgcn_wave_barrier();
-      WaveStore<kNt>(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N, lane);
+      WaveStoreAny<kWave * NR * N, kNt>(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N,
+                                        lane);
       __builtin_amdgcn_wave_barrier();
     } else {
       if (active) {
@@ -248,7 +287,8 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
         for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
       }
       __builtin_amdgcn_wave_barrier();
-      WaveStore<kNt>(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
+      WaveStoreAny<kWave * NR * S0, kNt>(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0,
+                                         nw * NR * S0, lane);
       __builtin_amdgcn_wave_barrier();
       if constexpr (S1 > 0) {
         if (active) {
@@ -256,7 +296,8 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
           for (int q = 0; q < NR * S1; ++q) st[lane * NR * S1 + q] = J1[q];
         }
         __builtin_amdgcn_wave_barrier();
-        WaveStore(st, a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0, nw * NR * S1, lane);
+        WaveStoreAny<kWave * NR * S1, kNt>(st, a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0,
+                                           nw * NR * S1, lane);
         __builtin_amdgcn_wave_barrier();
       }
     }
