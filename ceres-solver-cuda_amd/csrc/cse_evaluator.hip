@@ -140,6 +140,7 @@ LaunchFn SnavelyVariant(int v) {
     case 13: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, true>;
     case 14: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, true>;
     case 15: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, true>;
+    case 16: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, true>;
     default: return nullptr;
   }
 }

@@ -243,7 +243,7 @@ CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, d
 //       [jac_base[j][0] + stride_j*i0, + kR*size_j*nw)
 //   kCrs = true (CompressedRowSparseMatrix): whole blocks, kR rows of N
 //       columns, at [row0 + kR*N*i0, + kR*N*nw)
-template <class K, bool kJac, bool kCrs, bool kNt = true>
+template <class K, bool kJac, bool kCrs, bool kNt = true, bool kOneRound = false>
 __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
                                               int64_t i0, int nw, const double* r,
                                               const double* J0, const double* J1) {
@@ -251,13 +251,18 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
   constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
   if (nw <= 0) return;
   if (a.residuals) {
+    // Residuals are already lane-contiguous (kR doubles per block): each
+    // lane stores its own, no staging.
+    double* dst = a.residuals + a.res_base + (int64_t)NR * (i0 + lane);
     if (active) {
+      if (NR == 2 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        __builtin_nontemporal_store(r[0], dst);
+        __builtin_nontemporal_store(r[NR - 1], dst + 1);
+      } else {
 #pragma unroll
-      for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
+        for (int k = 0; k < NR; ++k) __builtin_nontemporal_store(r[k], dst + k);
+      }
     }
-    __builtin_amdgcn_wave_barrier();
-    WaveStoreAny<kWave * NR, kNt>(st, a.residuals + a.res_base + (int64_t)NR * i0, nw * NR, lane);
-    __builtin_amdgcn_wave_barrier();
   }
   if constexpr (kJac) {
     if (!a.jacobian) return;
@@ -280,6 +285,21 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
       __builtin_amdgcn_wave_barrier();
       WaveStoreAny<kWave * NR * N, kNt>(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N,
                                         lane);
+      __builtin_amdgcn_wave_barrier();
+    } else if constexpr (kOneRound && S1 > 0) {
+      // Both slots' cells staged at once, one LDS round trip.
+      double* st1 = st + kWave * NR * S0;
+      if (active) {
+#pragma unroll
+        for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
+#pragma unroll
+        for (int q = 0; q < NR * S1; ++q) st1[lane * NR * S1 + q] = J1[q];
+      }
+      __builtin_amdgcn_wave_barrier();
+      WaveStoreAny<kWave * NR * S0, kNt>(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0,
+                                         nw * NR * S0, lane);
+      WaveStoreAny<kWave * NR * S1, kNt>(st1, a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0,
+                                         nw * NR * S1, lane);
       __builtin_amdgcn_wave_barrier();
     } else {
       if (active) {
@@ -461,8 +481,9 @@ template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, 
 __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
-  constexpr int kOutLane =
-      !kStage ? 1 : kJac ? (kCrs ? NR * N : (NR * S0 > NR * S1 ? NR * S0 : NR * S1)) : NR;
+  constexpr int kOutLane = !kStage ? 1
+                          : kJac ? (kCrs || kDebug == 4 ? NR * N : (NR * S0 > NR * S1 ? NR * S0 : NR * S1))
+                                 : 1;
   // The staging buffer also holds the cooperative camera gather (used
   // before the outputs are staged).
   constexpr int kStageLane = kCoop && S0 > kOutLane ? S0 : kOutLane;
@@ -548,7 +569,8 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
     }
     if constexpr (kDebug == 2) {
     } else if constexpr (kStage) {
-      StageAndStore<K, kJac, kCrs, kDebug != 3>(a, st, lane, active, i0, nw, r, J0, J1);
+      StageAndStore<K, kJac, kCrs, kDebug != 3, kDebug == 4>(a, st, lane, active, i0, nw, r, J0,
+                                                             J1);
     } else if (active) {
       DirectStore<K, kJac, kCrs>(a, i0 + lane, r, J0, J1);
     }

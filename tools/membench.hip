@@ -108,12 +108,31 @@ __device__ __forceinline__ double coop_camera(const double* cams, int camid, int
   return s;
 }
 
-template <bool kPad, bool kWrite>
+// Outputs staged through LDS exactly as the evaluator does (lane-major
+// block values -> contiguous segments).
+__device__ __forceinline__ void write_chunk_staged(double* res, double* E, double* F, long c,
+                                                   int lane, double v, double* st) {
+  auto seg = [&](double* dst, int per_lane) {
+    for (int q = 0; q < per_lane; ++q) st[lane * per_lane + q] = v + q;
+    __builtin_amdgcn_wave_barrier();
+    for (int t = lane; t < 32 * per_lane; t += 64) {
+      const double2 x = reinterpret_cast<const double2*>(st)[t];
+      __builtin_nontemporal_store(x.x, dst + 2 * t);
+      __builtin_nontemporal_store(x.y, dst + 2 * t + 1);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  seg(res + 128 * c, 2);
+  seg(E + 384 * c, 6);
+  seg(F + 1152 * c, 18);
+}
+
+template <bool kPad, int kWrite, int kLdsPad = 0>
 __global__ __launch_bounds__(256) void coop_gather(const int2* ids, const double2* obs,
                                                    const double* state, const double* cam80,
                                                    double* res, double* E, double* F,
                                                    double* sink, long chunks, long n) {
-  __shared__ double lds[4][64 * 10];
+  __shared__ double lds[4][64 * (kWrite == 2 ? 18 : 10) + kLdsPad];
   const int lane = threadIdx.x & 63, wave = threadIdx.x / 64;
   const long stride = (long)gridDim.x * 4;
   double acc = 0.0;
@@ -126,7 +145,8 @@ __global__ __launch_bounds__(256) void coop_gather(const int2* ids, const double
     double v = o.x + o.y + pt[0] + pt[1] + pt[2];
     v += kPad ? coop_camera<true>(cam80, id.x, lane, lds[wave])
               : coop_camera<false>(state + 3L * kP, id.x, lane, lds[wave]);
-    if constexpr (kWrite) write_chunk<true>(res, E, F, c, lane, v);
+    if constexpr (kWrite == 1) write_chunk<true>(res, E, F, c, lane, v);
+    else if constexpr (kWrite == 2) write_chunk_staged(res, E, F, c, lane, v, lds[wave]);
     else acc += v;
   }
   if (acc == 12345.678) sink[0] = acc;
@@ -206,7 +226,7 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const long n2 = (128L + 384L + 1152L) * chunks / 2;
-  for (int wpc : {4, 8, 0}) {
+  for (int wpc : {0}) {
     const unsigned g = wpc ? (unsigned)(cus * wpc) : (unsigned)((chunks + 3) / 4);
     char nm[128];
     snprintf(nm, sizeof nm, "write_seq nt   grid=%u", g);
@@ -217,14 +237,18 @@ int main(int argc, char** argv) {
     run(nm, wbytes, [&] { hipLaunchKernelGGL(write_segs<false>, dim3(g), dim3(256), 0, 0, res, E, F, chunks); });
     snprintf(nm, sizeof nm, "read_gather    grid=%u", g);
     run(nm, rbytes, [&] { hipLaunchKernelGGL(read_gather, dim3(g), dim3(256), 0, 0, ids, obs, state, sink, (long)kO); });
+    snprintf(nm, sizeof nm, "coop72 +segs lds37K grid=%u", g);
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 1, 512>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    snprintf(nm, sizeof nm, "coop72 +staged   grid=%u", g);
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 2>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop72 read    grid=%u", g);
-    run(nm, rbytes, [&] { hipLaunchKernelGGL((coop_gather<false, false>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    run(nm, rbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 0>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop80 read    grid=%u", g);
-    run(nm, rbytes, [&] { hipLaunchKernelGGL((coop_gather<true, false>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    run(nm, rbytes, [&] { hipLaunchKernelGGL((coop_gather<true, 0>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop72 +segs   grid=%u", g);
-    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, true>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 1>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop80 +segs   grid=%u", g);
-    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<true, true>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<true, 1>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "gather_segs nt grid=%u", g);
     run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL(gather_segs<true>, dim3(g), dim3(256), 0, 0, ids, obs, state, res, E, F, chunks, (long)kO); });
   }
