@@ -94,6 +94,11 @@ struct Group {
   int64_t res_base = 0;
   int64_t jac_base[2][3] = {{0, 0, 0}, {0, 0, 0}};
   int64_t jac_stride[2] = {0, 0};
+  // Repacked slot-0 table (affine path, small id ranges).
+  int32_t slot0_lo = 0;
+  int64_t slot0_count = 0;
+  int slot0_stride = 0;
+  DevBuf<double> packed0;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -104,8 +109,8 @@ void LaunchGeneral(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
-template <class K, int L, bool J, bool Crs, int Pf = 2, bool St = true, int Mw = 0, int Dbg = 0,
-          bool Co = false>
+template <class K, int L, bool J, bool Crs, int Pf = -1, bool St = true, int Mw = 0, int Dbg = 4,
+          int Co = 2>
 void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (Mw == 0) {
     hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St, Dbg, Co>),
@@ -123,24 +128,26 @@ template <int L>
 LaunchFn SnavelyVariant(int v) {
   using K = cse::SnavelyKind;
   switch (v) {
-    case 1: return &LaunchAffine<K, L, true, false, 2, true, 3>;
-    case 2: return &LaunchAffine<K, L, true, false, 1, true, 0>;
-    case 3: return &LaunchAffine<K, L, true, false, 0, true, 0>;
-    case 4: return &LaunchAffine<K, L, true, false, 1, false, 0>;
-    case 5: return &LaunchAffine<K, L, true, false, 0, false, 0>;
-    case 6: return &LaunchAffine<K, L, true, false, 2, false, 0>;
-    case 7: return &LaunchAffine<K, L, true, false, 1, true, 4>;
-    case 8: return &LaunchAffine<K, L, true, false, -1, true, 0>;
-    case 9: return &LaunchAffine<K, L, true, false, -1, false, 0>;
+    case 1: return &LaunchAffine<K, L, true, false, 2, true, 3, 0, 0>;
+    case 2: return &LaunchAffine<K, L, true, false, 1, true, 0, 0, 0>;
+    case 3: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, 0>;
+    case 4: return &LaunchAffine<K, L, true, false, 1, false, 0, 0, 0>;
+    case 5: return &LaunchAffine<K, L, true, false, 0, false, 0, 0, 0>;
+    case 6: return &LaunchAffine<K, L, true, false, 2, false, 0, 0, 0>;
+    case 7: return &LaunchAffine<K, L, true, false, 1, true, 4, 0, 0>;
+    case 8: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, 0>;
+    case 9: return &LaunchAffine<K, L, true, false, -1, false, 0, 0, 0>;
     // Diagnostics (wrong results by design): memory floor, compute floor,
     // plain (not non-temporal) stores.
-    case 10: return &LaunchAffine<K, L, true, false, -1, true, 0, 1>;
-    case 11: return &LaunchAffine<K, L, true, false, -1, true, 0, 2>;
-    case 12: return &LaunchAffine<K, L, true, false, -1, true, 0, 3>;
-    case 13: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, true>;
-    case 14: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, true>;
-    case 15: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, true>;
-    case 16: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, true>;
+    case 10: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 0>;
+    case 11: return &LaunchAffine<K, L, true, false, -1, true, 0, 2, 0>;
+    case 12: return &LaunchAffine<K, L, true, false, -1, true, 0, 3, 0>;
+    case 13: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, 1>;
+    case 14: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 1>;
+    case 15: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, 1>;
+    case 16: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 1>;
+    case 17: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 2>;
+    case 18: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 2>;
     default: return nullptr;
   }
 }
@@ -154,25 +161,34 @@ int AffineVariant() {
 // 2 = affine interleaved rows (CRS).
 enum Policy { kTable = 0, kAffinePacked = 1, kAffineCrs = 2 };
 
+// Affine kernels: cooperative slot-0 gather by LDS-DMA from the repacked
+// table (dma = true) or by 8-byte pieces straight from the state.
+template <class K, int L, bool Crs>
+LaunchFn PickAffine(bool jac, bool dma) {
+  if (dma) return jac ? &LaunchAffine<K, L, true, Crs> : &LaunchAffine<K, L, false, Crs>;
+  return jac ? &LaunchAffine<K, L, true, Crs, -1, true, 0, 4, 1>
+             : &LaunchAffine<K, L, false, Crs, -1, true, 0, 4, 1>;
+}
+
 template <class K, int L>
-LaunchFn PickJP(bool jac, int policy) {
+LaunchFn PickJP(bool jac, int policy, bool dma) {
   switch (policy) {
-    case kAffinePacked: return jac ? &LaunchAffine<K, L, true, false> : &LaunchAffine<K, L, false, false>;
-    case kAffineCrs: return jac ? &LaunchAffine<K, L, true, true> : &LaunchAffine<K, L, false, true>;
+    case kAffinePacked: return PickAffine<K, L, false>(jac, dma);
+    case kAffineCrs: return PickAffine<K, L, true>(jac, dma);
     default: return jac ? &LaunchGeneral<K, L, true> : &LaunchGeneral<K, L, false>;
   }
 }
 
 template <class K>
-LaunchFn PickL(int loss, bool jac, int policy) {
+LaunchFn PickL(int loss, bool jac, int policy, bool dma) {
   switch (loss) {
-    case CSE_LOSS_HUBER: return PickJP<K, cse::kLossHuber>(jac, policy);
-    case CSE_LOSS_CAUCHY: return PickJP<K, cse::kLossCauchy>(jac, policy);
-    default: return PickJP<K, cse::kLossTrivial>(jac, policy);
+    case CSE_LOSS_HUBER: return PickJP<K, cse::kLossHuber>(jac, policy, dma);
+    case CSE_LOSS_CAUCHY: return PickJP<K, cse::kLossCauchy>(jac, policy, dma);
+    default: return PickJP<K, cse::kLossTrivial>(jac, policy, dma);
   }
 }
 
-LaunchFn Pick(int kind, int loss, bool jac, int policy) {
+LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
   const int v = AffineVariant();
   if (v > 0 && kind == CSE_FUNCTOR_SNAVELY_2_9_3 && jac && policy == kAffinePacked) {
     LaunchFn f = loss == CSE_LOSS_HUBER ? SnavelyVariant<cse::kLossHuber>(v)
@@ -180,13 +196,13 @@ LaunchFn Pick(int kind, int loss, bool jac, int policy) {
     if (f) return f;
   }
   switch (kind) {
-    case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, policy);
+    case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, policy, dma);
     case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3:
-      return PickL<cse::SnavelyNoDistortionKind>(loss, jac, policy);
+      return PickL<cse::SnavelyNoDistortionKind>(loss, jac, policy, dma);
     case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3:
-      return PickL<cse::SnavelyQuaternionKind>(loss, jac, policy);
+      return PickL<cse::SnavelyQuaternionKind>(loss, jac, policy, dma);
     case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3:
-      return PickL<cse::PointDisplacementKind>(loss, jac, policy);
+      return PickL<cse::PointDisplacementKind>(loss, jac, policy, dma);
     default: return nullptr;
   }
 }
@@ -201,7 +217,7 @@ int PersistentWgPerCu(const KindShape& k, int policy) {
     if (v == 0) return 1 << 20;  // one chunk per wave: not persistent
   }
   const int v = AffineVariant();
-  if (v >= 8 && v != 15) return 1 << 20;  // the non-persistent variants
+  if (v == 0 || (v >= 8 && v != 15)) return 1 << 20;  // the non-persistent variants
   const int lane_doubles = policy == kAffineCrs ? k.nr * (k.s0 + k.s1)
                                                 : k.nr * std::max(k.s0, k.s1);
   const int lds = cse::kWavesPerBlock * cse::kWave * lane_doubles * 8 + 64;
@@ -304,6 +320,15 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
       if (pb.state_offset != G->state_base[j] + (int64_t)sizes[j] * id) return kTable;
       if (pb.delta_offset != G->delta_base[j] + (int64_t)sizes[j] * id) return kTable;
     }
+  // Slot-0 id range (the repacked table of the cooperative gather).
+  int32_t lo = g.parameter_block_ids[0], hi = lo;
+  for (int64_t i = 0; i < n; ++i) {
+    lo = std::min(lo, g.parameter_block_ids[i * k.nb]);
+    hi = std::max(hi, g.parameter_block_ids[i * k.nb]);
+  }
+  G->slot0_lo = lo;
+  G->slot0_count = (int64_t)hi - lo + 1;
+  G->slot0_stride = (k.s0 + 1) & ~1;
   // Residuals.
   G->res_base = d->residual_layout[gidx(0)];
   for (int64_t i = 0; i < n; ++i)
@@ -366,6 +391,9 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
     for (int r = 0; r < 3; ++r) a.jac_base[j][r] = G.jac_base[j][r];
   }
   a.res_base = G.res_base;
+  a.packed0 = G.packed0.p;
+  a.packed0_lo = G.slot0_lo;
+  a.packed0_stride = G.slot0_stride;
   a.gindex = G.gindex.p;
   a.first = G.first;
   a.residual_layout = ev->res_layout.p;
@@ -427,10 +455,17 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
   for (size_t g = 0; g < ev->groups.size(); ++g) {
     Group& G = ev->groups[g];
     if (G.n == 0) continue;
-    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy);
+    const bool dma = G.packed0.p != nullptr;
+    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma);
     if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
     const cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, d_grad);
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
+    if (dma) {
+      const int64_t total = G.slot0_count * G.slot0_stride;
+      hipLaunchKernelGGL(cse::RepackSlot0Kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                         ev->stream, d_state, G.state_base[0], G.shape.s0, G.slot0_stride,
+                         G.slot0_lo, G.slot0_count, G.packed0.p);
+    }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
   }
@@ -578,6 +613,13 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     }
     G.partial_offset = ev->total_wg;
     ev->total_wg += G.num_wg;
+    // The LDS-DMA gather reads slot 0 from a repacked copy refreshed every
+    // evaluation; worth it while the slot-0 id range is small (BAL: the
+    // cameras), otherwise gather 8-byte pieces from the state directly.
+    if (G.affine && G.slot0_count > 0 && G.slot0_count <= (1 << 20) &&
+        getenv("CSE_NO_DMA_GATHER") == nullptr &&
+        (rc = G.packed0.alloc((size_t)G.slot0_count * G.slot0_stride)))
+      return bail(rc);
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
     if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
     if (!G.affine && g.residual_block_index &&
@@ -689,6 +731,7 @@ void cse_destroy(cse_evaluator* ev) {
   (void)hipSetDevice(ev->device);
   if (ev->stream) (void)hipStreamSynchronize(ev->stream);
   for (auto& G : ev->groups) {
+    G.packed0.release();
     G.ids.release();
     G.data.release();
     G.gindex.release();

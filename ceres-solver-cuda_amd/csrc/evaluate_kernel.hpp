@@ -66,6 +66,11 @@ struct GroupArgs {
   int64_t res_base;
   int64_t jac_base[2][3];
   int64_t jac_stride[2];
+  // Slot-0 parameter blocks repacked at a 16-byte-aligned stride (the
+  // affine path's cooperative LDS-DMA gather; see RepackSlot0Kernel).
+  const double* packed0;
+  int32_t packed0_lo;
+  int32_t packed0_stride;  // doubles per block, even
   // Table policy.
   const int64_t* gindex;
   int64_t first;
@@ -468,6 +473,49 @@ __device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 i
   in->id1 = id.y;
 }
 
+// Same gather with slot 0 fetched by LDS-DMA (global_load_lds_dwordx4):
+// slot-0 blocks are read from the 16-byte-aligned repacked table, piece p
+// (16 B) of the wave's 64 blocks by lane p % 64 of load p / 64; the
+// hardware writes each lane's 16 B at lds + 16 * p, so the pieces land in
+// block order without passing through VGPRs.
+template <class K>
+__device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int2 id,
+                                              AffineInputs<K>* in, double* lds, int lane) {
+  using Tr = KindTraits<K>;
+  constexpr int S0 = Tr::S0, S1 = Tr::S1, D = Tr::D;
+  constexpr int S0p = (S0 + 1) & ~1;  // doubles per block in the packed table
+  constexpr int kPieces = S0p / 2;    // 16-byte pieces per block
+  const int cid_own = id.x - a.packed0_lo;
+#pragma unroll
+  for (int k = 0; k < kPieces; ++k) {
+    const int p = k * kWave + lane;
+    const int t = p / kPieces, q = p - t * kPieces;
+    const int cid = __shfl(cid_own, t, kWave);
+    const double* src = a.packed0 + (int64_t)S0p * cid + 2 * q;
+    __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
+  }
+  if constexpr (D == 2) {
+    const double2 v = *reinterpret_cast<const double2*>(a.data + 2 * i);
+    in->d[0] = v.x;
+    in->d[1] = v.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) in->d[k] = a.data[i * D + k];
+  }
+  if constexpr (S1 > 0) {
+    const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < S1; ++k) in->x1[k] = p1[k];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+  __builtin_amdgcn_wave_barrier();
+  in->id0 = id.x;
+  in->id1 = id.y;
+}
+
 // The hot path: persistent, software-pipelined, table-free.
 //   kPrefetch 2: gathers of chunk c+1 and ids of chunk c+2 in flight while
 //                chunk c computes; 1: only the ids of chunk c+1; 0: none;
@@ -477,7 +525,7 @@ __device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 i
 //   map of its inputs (memory-path floor), 2 skips the stores (compute
 //   floor), 3 stores without the non-temporal hint.
 template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0,
-          bool kCoop = false>
+          int kCoop = 0>
 __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
@@ -486,7 +534,8 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
                                  : 1;
   // The staging buffer also holds the cooperative camera gather (used
   // before the outputs are staged).
-  constexpr int kStageLane = kCoop && S0 > kOutLane ? S0 : kOutLane;
+  constexpr int kCoopLane = kCoop == 2 ? ((S0 + 1) & ~1) : kCoop == 1 ? S0 : 0;
+  constexpr int kStageLane = kCoopLane > kOutLane ? kCoopLane : kOutLane;
   __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
   __shared__ double lds_sum[kWavesPerBlock];
 
@@ -522,7 +571,9 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
     } else if constexpr (kPrefetch == 1) {
       Gather<K>(a, idx(c), ids_next, &cur);
       if (cn < num_chunks) ids_next = LoadIds<K>(a, idx(cn));
-    } else if constexpr (kCoop) {
+    } else if constexpr (kCoop == 2) {
+      GatherCoopDma<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur, st, lane);
+    } else if constexpr (kCoop == 1) {
       GatherCoop<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur, st, lane);
     } else {
       Gather<K>(a, idx(c), LoadIds<K>(a, idx(c)), &cur);
@@ -589,7 +640,7 @@ __global__ __launch_bounds__(kBlockThreads, kMinWaves) void EvaluateAffinePersis
 
 // Same kernel without an occupancy request (the compiler's default target).
 template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kDebug = 0,
-          bool kCoop = false>
+          int kCoop = 0>
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffinePersistentD(const GroupArgs a) {
   AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage, kDebug, kCoop>(a);
 }
@@ -734,8 +785,18 @@ __global__ __launch_bounds__(1024) void FinalizeKernel(const double* partials, i
                                                        double* cost, int* status,
                                                        int* status_out) {
   __shared__ double wsum[1024 / kWave];
-  double v = 0.0;
-  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) v += partials[k];
+  // Four independent accumulators per thread keep several loads in flight.
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+  const int64_t step = blockDim.x;
+  int64_t k = threadIdx.x;
+  for (; k + 3 * step < n; k += 4 * step) {
+    v0 += partials[k];
+    v1 += partials[k + step];
+    v2 += partials[k + 2 * step];
+    v3 += partials[k + 3 * step];
+  }
+  for (; k < n; k += step) v0 += partials[k];
+  double v = (v0 + v1) + (v2 + v3);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = v;
@@ -748,6 +809,19 @@ __global__ __launch_bounds__(1024) void FinalizeKernel(const double* partials, i
     *status_out = s;
     *status = 0;
   }
+}
+
+// Copies slot-0 parameter blocks [lo, lo + count) of the state into the
+// packed table at a 16-byte-aligned stride (once per evaluation: 13,682
+// cameras = 1.1 MB for BAL problem-13682).
+__global__ __launch_bounds__(256) void RepackSlot0Kernel(const double* state, int64_t state_base,
+                                                         int size, int stride, int32_t lo,
+                                                         int64_t count, double* packed) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = t / stride;
+  const int k = (int)(t - b * stride);
+  if (b >= count) return;
+  packed[t] = k < size ? state[state_base + (int64_t)size * (lo + b) + k] : 0.0;
 }
 
 }  // namespace cse

@@ -127,12 +127,46 @@ __device__ __forceinline__ void write_chunk_staged(double* res, double* E, doubl
   seg(F + 1152 * c, 18);
 }
 
+// LDS round trip of the same volume, but the global stores do not depend
+// on it (isolates LDS/VGPR-export contention from the store path).
+__device__ __forceinline__ double lds_roundtrip(int lane, double v, double* st) {
+  double acc = 0.0;
+#pragma unroll
+  for (int q = 0; q < 24; ++q) st[lane * 24 + q] = v + q;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int q = 0; q < 24; ++q) acc += st[(q * 64 + lane) % (64 * 24)];
+  __builtin_amdgcn_wave_barrier();
+  return acc;
+}
+
+// Per-lane (unstaged) stores at the block stride: E 48 B, F 144 B per lane.
+__device__ __forceinline__ void write_chunk_strided(double* res, double* E, double* F, long c,
+                                                    int lane, double v, bool stage_f, double* st) {
+  st16<true>(res + 128 * c + 2 * lane, v, v);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st16<true>(E + 384 * c + 6 * lane + 2 * k, v, v);
+  if (stage_f) {
+    for (int q = 0; q < 18; ++q) st[lane * 18 + q] = v + q;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const double2 x = reinterpret_cast<const double2*>(st)[k * 64 + lane];
+      st16<true>(F + 1152 * c + 128 * k + 2 * lane, x.x, x.y);
+    }
+    __builtin_amdgcn_wave_barrier();
+  } else {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) st16<true>(F + 1152 * c + 18 * lane + 2 * k, v, v);
+  }
+}
+
 template <bool kPad, int kWrite, int kLdsPad = 0>
 __global__ __launch_bounds__(256) void coop_gather(const int2* ids, const double2* obs,
                                                    const double* state, const double* cam80,
                                                    double* res, double* E, double* F,
                                                    double* sink, long chunks, long n) {
-  __shared__ double lds[4][64 * (kWrite == 2 ? 18 : 10) + kLdsPad];
+  __shared__ double lds[4][64 * (kWrite >= 2 ? 24 : 10) + kLdsPad];
   const int lane = threadIdx.x & 63, wave = threadIdx.x / 64;
   const long stride = (long)gridDim.x * 4;
   double acc = 0.0;
@@ -147,6 +181,9 @@ __global__ __launch_bounds__(256) void coop_gather(const int2* ids, const double
               : coop_camera<false>(state + 3L * kP, id.x, lane, lds[wave]);
     if constexpr (kWrite == 1) write_chunk<true>(res, E, F, c, lane, v);
     else if constexpr (kWrite == 2) write_chunk_staged(res, E, F, c, lane, v, lds[wave]);
+    else if constexpr (kWrite == 3) write_chunk<true>(res, E, F, c, lane, v + lds_roundtrip(lane, v, lds[wave]));
+    else if constexpr (kWrite == 4) write_chunk_strided(res, E, F, c, lane, v, false, lds[wave]);
+    else if constexpr (kWrite == 5) write_chunk_strided(res, E, F, c, lane, v, true, lds[wave]);
     else acc += v;
   }
   if (acc == 12345.678) sink[0] = acc;
@@ -241,6 +278,12 @@ int main(int argc, char** argv) {
     run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 1, 512>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop72 +staged   grid=%u", g);
     run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 2>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    snprintf(nm, sizeof nm, "coop72 +lds-indep+segs grid=%u", g);
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 3>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    snprintf(nm, sizeof nm, "coop72 +strided E,F    grid=%u", g);
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 4>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
+    snprintf(nm, sizeof nm, "coop72 +strided E, staged F grid=%u", g);
+    run(nm, rbytes + wbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 5>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop72 read    grid=%u", g);
     run(nm, rbytes, [&] { hipLaunchKernelGGL((coop_gather<false, 0>), dim3(g), dim3(256), 0, 0, ids, obs, state, cam80, res, E, F, sink, chunks, (long)kO); });
     snprintf(nm, sizeof nm, "coop80 read    grid=%u", g);
