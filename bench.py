@@ -34,7 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
 
 import ceres_amd as ca  # noqa: E402
-from ceres_amd import bal  # noqa: E402
+from ceres_amd import bal, shard  # noqa: E402
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "residual+Jacobian evaluations/sec on BAL problem-13682; achieved HBM GB/s"
@@ -62,21 +62,6 @@ def make_loss(name):
             "cauchy": ca.Loss.cauchy(1.0)}[name]
 
 
-def point_bucket_cuts(pt_idx, num_points, world):
-    """Shard boundaries over residual blocks at point-bucket boundaries
-    (SURVEY.md §8(e)): rank r gets points [pc[r], pc[r+1]) and the blocks
-    [bc[r], bc[r+1]) observing them."""
-    counts = np.bincount(pt_idx, minlength=num_points)
-    csum = np.concatenate([[0], np.cumsum(counts)])
-    O = int(csum[-1])
-    pc = [0]
-    for r in range(1, world):
-        pc.append(int(np.searchsorted(csum, O * r // world)))
-    pc.append(num_points)
-    bc = [int(csum[p]) for p in pc]
-    return pc, bc
-
-
 def build_shard(args, rank, world):
     counts = bal.CONFIGS[args.config]
     loss = make_loss(args.loss)
@@ -85,14 +70,10 @@ def build_shard(args, rank, world):
         prog = bal.program(cams, pts, ci, pi, obs, loss=loss, format=args.format)
         return prog, {"blocks": int(counts[2]), "strip": None}
     cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed)
-    pc, bc = point_bucket_cuts(pi, pts.shape[0], world)
-    p0, p1, b0, b1 = pc[rank], pc[rank + 1], bc[rank], bc[rank + 1]
-    prog = bal.program(cams, pts[p0:p1], ci[b0:b1], pi[b0:b1] - p0, obs[b0:b1], loss=loss,
-                       format=args.format)
-    O = int(counts[2])
-    strip = ({"E": [6 * b0, 6 * b1], "F": [6 * O + 18 * b0, 6 * O + 18 * b1]}
-             if args.format == "block_sparse" else {"rows": [24 * b0, 24 * b1]})
-    return prog, {"blocks": b1 - b0, "strip": strip}
+    prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss,
+                                   format=args.format)
+    strips = [[g, g + n] for _, g, n in sh.jacobian_strips()]
+    return prog, {"blocks": sh.blocks[1] - sh.blocks[0], "strip": strips}
 
 
 def cpu_baseline(args, threads):
@@ -145,7 +126,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     t_build = time.perf_counter()
-    prog, shard = build_shard(args, rank, world)
+    prog, shard_info = build_shard(args, rank, world)
     build_s = time.perf_counter() - t_build
 
     stream = torch.cuda.current_stream(dev)
@@ -230,10 +211,10 @@ def main():
                             f"{args.loss} {args.format} residual+Jacobian"
                             f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
-                "blocks_per_rank": shard["blocks"],
+                "blocks_per_rank": shard_info["blocks"],
                 "parallelism": ("replica shards per rank" if weak and world > 1 else
                                 "point-bucket block sharding" if world > 1 else "single GPU"),
-                "strip_rank0": shard["strip"],
+                "strip_rank0": shard_info["strip"],
             },
             "roofline": {
                 "bound": "hbm",

@@ -1,0 +1,111 @@
+"""Multi-process sharding on CPU with the gloo backend.
+
+Each rank builds its shard of the same synthetic BAL problem with
+ceres_amd.shard (point-bucket-aligned block ranges), evaluates it with the
+CPU oracle (these tests run without a GPU; on the GPU box bench.py runs the
+same shards through libcse.so and RCCL), all-reduces the cost and the camera
+gradient, and gathers its Jacobian/residual strips.  Rank 0 checks that the
+assembled strips and reduced values equal the unsharded evaluation.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, fmt, q):
+    import sys
+    for p in (os.path.join(REPO, "ceres-solver-cuda_amd"), os.path.join(REPO, "oracle"),
+              os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    import ceres_amd as ca
+    from ceres_amd import bal, shard
+    import oracle_py as O
+    from parity_util import is_approx
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        C, P, Obs = 12, 700, 2600
+        cams, pts, ci, pi, obs = bal.synthetic(C, P, Obs, seed=21)
+        loss = ca.Loss.huber(1.0)
+        prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss, format=fmt)
+        ok, cost, r, g, j = O.OracleProgram.from_program(prog).evaluate(prog.state, num_threads=2)
+        assert ok
+        c = torch.tensor([cost], dtype=torch.float64)
+        dist.all_reduce(c)
+        pmap, cmap = shard.gradient_maps(sh, P, C)
+        gcam = torch.from_numpy(g[cmap[0]:cmap[0] + cmap[2]].copy())
+        dist.all_reduce(gcam)
+        parts = [None] * world
+        dist.all_gather_object(parts, (sh, r, j, g[pmap[0]:pmap[0] + pmap[2]].copy()))
+        if rank == 0:
+            full = bal.program(cams, pts, ci, pi, obs, loss=loss, format=fmt)
+            okf, costf, rf, gf, jf = O.OracleProgram.from_program(full).evaluate(full.state,
+                                                                              num_threads=2)
+            assert okf
+            assert abs(float(c.item()) - costf) <= 1e-12 * abs(costf)
+            J = shard.assemble([p[0] for p in parts], [p[2] for p in parts], full.num_jacobian_values)
+            assert not np.isnan(J).any()
+            # Same per-block arithmetic on each side: the strips are bitwise equal.
+            assert np.array_equal(J, jf)
+            R = np.concatenate([p[1] for p in parts])
+            assert np.array_equal(R, rf)
+            G = np.concatenate([p[3] for p in parts] + [gcam.numpy()])
+            assert is_approx(G, gf, 1e-13)
+            sizes = [p[0].blocks[1] - p[0].blocks[0] for p in parts]
+            assert sum(sizes) == Obs and max(sizes) - min(sizes) <= 2 * (Obs // P + 1)
+        q.put((rank, "ok"))
+    except Exception as e:  # report to the parent
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("fmt", ["block_sparse", "compressed_row"])
+def test_sharded_evaluation_matches_unsharded(world, fmt):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    results = dict(q.get() for _ in range(world))
+    assert all(v == "ok" for v in results.values()), results
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_point_bucket_cuts_properties():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
+    from ceres_amd import shard
+    rng = np.random.default_rng(0)
+    pt = np.sort(rng.integers(0, 1000, 20000))
+    for world in (1, 2, 4, 8, 7):
+        pc, bc = shard.point_bucket_cuts(pt, 1000, world)
+        assert pc[0] == 0 and pc[-1] == 1000 and bc[0] == 0 and bc[-1] == len(pt)
+        assert all(a <= b for a, b in zip(bc, bc[1:]))
+        for r in range(1, world):
+            # a cut never splits a point's observations
+            if 0 < bc[r] < len(pt):
+                assert pt[bc[r] - 1] < pt[bc[r]]
+    with pytest.raises(ValueError):
+        shard.point_bucket_cuts(pt[::-1], 1000, 2)
