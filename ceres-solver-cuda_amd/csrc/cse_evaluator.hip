@@ -103,6 +103,11 @@ struct Group {
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
 
+// Cost reduction: above this many per-workgroup partials, a first pass of
+// kPartialBlocks workgroups shortens the serial tail of FinalizeKernel.
+constexpr int64_t kPartialsTwoPass = 4096;
+constexpr int kPartialBlocks = 128;
+
 template <class K, int L, bool J>
 void LaunchGeneral(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   hipLaunchKernelGGL((cse::EvaluateGroupKernel<K, L, J>), dim3((unsigned)num_wg),
@@ -245,7 +250,7 @@ struct cse_evaluator {
   DevBuf<cse::PbDev> pbs;
   DevBuf<double> cstate, plus_jac;
   DevBuf<int64_t> res_layout, jac_layout, jac_offsets;
-  DevBuf<double> partials;
+  DevBuf<double> partials, partials2;
   DevBuf<int> status;  // [0] running flag, [1] last status
   // Host-path buffers (allocated on first use).
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
@@ -474,9 +479,18 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     CSE_HIP(hipEventRecord(timing.second, ev->stream));
     ev->pending.push_back(timing);
   }
-  hipLaunchKernelGGL(cse::FinalizeKernel, dim3(1), dim3(1024), 0, ev->stream,
-                     (const double*)ev->partials.p, ev->total_wg, d_cost, ev->status.p,
-                     ev->status.p + 1);
+  const double* parts = ev->partials.p;
+  int64_t nparts = ev->total_wg;
+  if (nparts > kPartialsTwoPass) {
+    // Two-pass, still fixed-order: kPartialBlocks sums, then one.
+    const int64_t per = (nparts + kPartialBlocks - 1) / kPartialBlocks;
+    hipLaunchKernelGGL(cse::PartialSumKernel, dim3(kPartialBlocks), dim3(cse::kBlockThreads), 0,
+                       ev->stream, parts, nparts, per, ev->partials2.p);
+    parts = ev->partials2.p;
+    nparts = kPartialBlocks;
+  }
+  hipLaunchKernelGGL(cse::FinalizeKernel, dim3(1), dim3(1024), 0, ev->stream, parts, nparts,
+                     d_cost, ev->status.p, ev->status.p + 1);
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }
@@ -652,6 +666,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     }
   }
   if ((rc = ev->partials.alloc(std::max<int64_t>(ev->total_wg, 1)))) return bail(rc);
+  if ((rc = ev->partials2.alloc(kPartialBlocks))) return bail(rc);
   if ((rc = ev->status.alloc(2))) return bail(rc);
   if (hipMemsetAsync(ev->status.p, 0, 2 * sizeof(int), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "memset failed"));
@@ -743,6 +758,7 @@ void cse_destroy(cse_evaluator* ev) {
   ev->jac_layout.release();
   ev->jac_offsets.release();
   ev->partials.release();
+  ev->partials2.release();
   ev->status.release();
   ev->h_state.release();
   ev->h_cost.release();

@@ -777,6 +777,20 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateGroupKernel(const Group
   if (threadIdx.x == 0) a.partials[blockIdx.x] = t;
 }
 
+// First pass of the cost reduction when there are many partials: workgroup
+// b sums partials [b*per, (b+1)*per) in a fixed order.
+__global__ __launch_bounds__(kBlockThreads) void PartialSumKernel(const double* partials,
+                                                                  int64_t n, int64_t per,
+                                                                  double* out) {
+  __shared__ double lds_sum[kWavesPerBlock];
+  const int64_t begin = (int64_t)blockIdx.x * per;
+  const int64_t end = begin + per < n ? begin + per : n;
+  double v = 0.0;
+  for (int64_t k = begin + threadIdx.x; k < end; k += kBlockThreads) v += partials[k];
+  const double t = WorkgroupSum(v, lds_sum);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
+}
+
 // Sums the per-workgroup partials of every group in a fixed order, writes
 // the cost, publishes the evaluation status and re-arms the status word
 // for the next evaluation (replaces thrust::reduce + the abort-flag round

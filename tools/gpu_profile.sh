@@ -17,7 +17,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD 
   timeout -k 10 300 rocprofv3 --pmc $group -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/pmc$i.log 2>&1 || echo "pmc group $i failed" >> $OUT/errors.txt
 done
 for d in $OUT/trace $OUT/pmc*; do
-  [ -d "$d" ] && python3 tools/pmc_summary.py "$d" EvaluateGroupKernel --json $OUT/summary.json > /dev/null
+  [ -d "$d" ] && python3 tools/pmc_summary.py "$d" EvaluateAffine --json $OUT/summary.json > /dev/null
 done
-python3 tools/pmc_summary.py $OUT/trace EvaluateGroupKernel > $OUT/trace_summary.json
+python3 tools/pmc_summary.py $OUT/trace EvaluateAffine > $OUT/trace_summary.json
 cat $OUT/summary.json
