@@ -126,6 +126,19 @@ void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   }
 }
 
+// The shipped affine kernel: one chunk per wave, back-to-back store tail.
+template <class K, int L, bool J, bool Crs, int Co, bool Two = false, int Dbg = 0>
+void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, Two, Dbg>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
+}
+
+template <int kStep>
+void LaunchM1(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL(cse::MembenchM1Kernel<kStep>, dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
+}
+
 // Tuning variants of the hot kernel (Snavely, Huber/Trivial, BSM,
 // Jacobian), selected by $CSE_AFFINE_VARIANT: (prefetch, LDS staging,
 // min waves per SIMD).
@@ -153,6 +166,33 @@ LaunchFn SnavelyVariant(int v) {
     case 16: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 1>;
     case 17: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 2>;
     case 18: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 2>;
+    case 19: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 2>;  // round-1 default
+    case 20: return &LaunchChunks<K, L, true, false, 2, true>;  // two-round staging
+    case 21: return &LaunchChunks<K, L, true, false, 2, false, 1>;  // memory floor
+    case 22: return &LaunchChunks<K, L, true, false, 2, false, 2>;  // compute floor
+    case 23: return &LaunchChunks<K, L, true, false, 2, false, 5>;  // memory floor, no transpose
+    case 24: return &LaunchChunks<K, L, true, false, 1, false, 1>;  // memory floor, register gather
+    case 25: return &LaunchChunks<K, L, true, false, 1, false, 5>;  // both
+    case 26: return &LaunchChunks<K, L, true, false, 2, false, 4>;  // real compute, no transpose
+    case 27: return &LaunchChunks<K, L, true, false, 2, false, 9>;  // memory floor, one data quad
+    case 28: return &LaunchChunks<K, L, true, false, 1, false, 9>;  // same, register gather
+    case 29: return &LaunchM1<0>;  // membench m1 memory path on the real buffers
+    case 30: return &LaunchM1<1>;  // + shipped store tail
+    case 31: return &LaunchM1<2>;  // + LDS-DMA gather
+    case 32: return &LaunchM1<3>;  // + distinct store data
+    case 33: return &LaunchChunks<K, L, true, false, 3>;          // register gather, packed
+    case 34: return &LaunchChunks<K, L, true, false, 3, true>;    // + two-round staging
+    case 35: return &LaunchChunks<K, L, true, false, 1>;          // 8-byte register gather
+    // Store cache policies (default 0 = nt sc1; see StoreNt16).
+    case 36: return &LaunchChunks<K, L, true, false, 2, false, 16>;  // plain stores
+    case 37: return &LaunchChunks<K, L, true, false, 2, false, 32>;  // sc1
+    case 38: return &LaunchChunks<K, L, true, false, 2, false, 48>;  // sc0 sc1
+    case 39: return &LaunchChunks<K, L, true, false, 2, false, 64>;  // nt (round-2 first cut)
+    case 40: return &LaunchChunks<K, L, true, false, 2, false, 80>;  // sc0 sc1 nt
+    case 41: return &LaunchChunks<K, L, true, false, 2, false, 96>;  // sc0 nt
+    case 42: return &LaunchChunks<K, L, true, false, 3>;             // register gather
+    case 43: return &LaunchChunks<K, L, true, false, 2, true>;       // two-round
+    case 44: return &LaunchChunks<K, L, true, false, 2, false, 512>; // plain (not nt) loads
     default: return nullptr;
   }
 }
@@ -170,9 +210,8 @@ enum Policy { kTable = 0, kAffinePacked = 1, kAffineCrs = 2 };
 // table (dma = true) or by 8-byte pieces straight from the state.
 template <class K, int L, bool Crs>
 LaunchFn PickAffine(bool jac, bool dma) {
-  if (dma) return jac ? &LaunchAffine<K, L, true, Crs> : &LaunchAffine<K, L, false, Crs>;
-  return jac ? &LaunchAffine<K, L, true, Crs, -1, true, 0, 4, 1>
-             : &LaunchAffine<K, L, false, Crs, -1, true, 0, 4, 1>;
+  if (dma) return jac ? &LaunchChunks<K, L, true, Crs, 2> : &LaunchChunks<K, L, false, Crs, 2>;
+  return jac ? &LaunchChunks<K, L, true, Crs, 1> : &LaunchChunks<K, L, false, Crs, 1>;
 }
 
 template <class K, int L>
@@ -625,8 +664,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     } else {
       G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
     }
+    // Every kernel writes one cost partial per wave.
     G.partial_offset = ev->total_wg;
-    ev->total_wg += G.num_wg;
+    ev->total_wg += G.num_wg * cse::kWavesPerBlock;
     // The LDS-DMA gather reads slot 0 from a repacked copy refreshed every
     // evaluation; worth it while the slot-0 id range is small (BAL: the
     // cameras), otherwise gather 8-byte pieces from the state directly.
@@ -666,6 +706,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     }
   }
   if ((rc = ev->partials.alloc(std::max<int64_t>(ev->total_wg, 1)))) return bail(rc);
+  // Slots of groups that launch nothing (empty groups) must read as zero.
+  if (hipMemsetAsync(ev->partials.p, 0, ev->partials.n * sizeof(double), s) != hipSuccess)
+    return bail(Fail(CSE_ERR_HIP, "hipMemsetAsync failed"));
   if ((rc = ev->partials2.alloc(kPartialBlocks))) return bail(rc);
   if ((rc = ev->status.alloc(2))) return bail(rc);
   if (hipMemsetAsync(ev->status.p, 0, 2 * sizeof(int), s) != hipSuccess)

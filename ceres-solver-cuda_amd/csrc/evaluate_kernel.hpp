@@ -473,12 +473,53 @@ __device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 i
   in->id1 = id.y;
 }
 
+// Cooperative slot-0 gather in 16-byte pieces through VGPRs from the
+// repacked table (the register twin of GatherCoopDma).
+template <class K>
+__device__ __forceinline__ void GatherCoopPacked(const GroupArgs& a, int64_t i, int2 id,
+                                                 AffineInputs<K>* in, double* lds, int lane) {
+  using Tr = KindTraits<K>;
+  constexpr int S0 = Tr::S0, S1 = Tr::S1, D = Tr::D;
+  constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kPieces = S0p / 2;
+  const int cid_own = id.x - a.packed0_lo;
+  double2 piece[kPieces];
+#pragma unroll
+  for (int k = 0; k < kPieces; ++k) {
+    const int p = k * kWave + lane;
+    const int t = p / kPieces, q = p - t * kPieces;
+    const int cid = __shfl(cid_own, t, kWave);
+    piece[k] = *reinterpret_cast<const double2*>(a.packed0 + (int64_t)S0p * cid + 2 * q);
+  }
+  if constexpr (D == 2) {
+    const double2 v = *reinterpret_cast<const double2*>(a.data + 2 * i);
+    in->d[0] = v.x;
+    in->d[1] = v.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) in->d[k] = a.data[i * D + k];
+  }
+  if constexpr (S1 > 0) {
+    const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < S1; ++k) in->x1[k] = p1[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kPieces; ++k) reinterpret_cast<double2*>(lds)[k * kWave + lane] = piece[k];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+  __builtin_amdgcn_wave_barrier();
+  in->id0 = id.x;
+  in->id1 = id.y;
+}
+
 // Same gather with slot 0 fetched by LDS-DMA (global_load_lds_dwordx4):
 // slot-0 blocks are read from the 16-byte-aligned repacked table, piece p
 // (16 B) of the wave's 64 blocks by lane p % 64 of load p / 64; the
 // hardware writes each lane's 16 B at lds + 16 * p, so the pieces land in
 // block order without passing through VGPRs.
-template <class K>
+template <class K, bool kNtLoads = false>
 __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int2 id,
                                               AffineInputs<K>* in, double* lds, int lane) {
   using Tr = KindTraits<K>;
@@ -494,7 +535,10 @@ __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int
     const double* src = a.packed0 + (int64_t)S0p * cid + 2 * q;
     __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
   }
-  if constexpr (D == 2) {
+  if constexpr (kNtLoads) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) in->d[k] = __builtin_nontemporal_load(a.data + i * D + k);
+  } else if constexpr (D == 2) {
     const double2 v = *reinterpret_cast<const double2*>(a.data + 2 * i);
     in->d[0] = v.x;
     in->d[1] = v.y;
@@ -505,7 +549,8 @@ __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int
   if constexpr (S1 > 0) {
     const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
 #pragma unroll
-    for (int k = 0; k < S1; ++k) in->x1[k] = p1[k];
+    for (int k = 0; k < S1; ++k)
+      in->x1[k] = kNtLoads ? __builtin_nontemporal_load(p1 + k) : p1[k];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
@@ -629,7 +674,10 @@ __device__ __forceinline__ void AffinePersistentBody(const GroupArgs& a) {
   }
   if (!all_ok) *a.status = 1;
   const double t = WorkgroupSum(cost_acc, lds_sum);
-  if (threadIdx.x == 0) a.partials[blockIdx.x] = t;
+  // Affine groups own kWavesPerBlock partial slots per workgroup
+  // (EvaluateAffineChunks writes one per wave).
+  if (threadIdx.x < kWavesPerBlock)
+    a.partials[(int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x] = threadIdx.x == 0 ? t : 0.0;
 }
 
 template <class K, int kLoss, bool kJac, bool kCrs, int kPrefetch, bool kStage, int kMinWaves>
@@ -645,13 +693,494 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateAffinePersistentD(const
   AffinePersistentBody<K, kLoss, kJac, kCrs, kPrefetch, kStage, kDebug, kCoop>(a);
 }
 
+// ---------------------------------------------------------------------------
+// The shipped hot kernel: one 64-block chunk per wave, every output store
+// issued back to back at the very end of the wave.
+//
+// Why the tail is shaped this way (measured, tools/membench2.hip): on
+// gfx950 a vector-memory store reads its address and data VGPRs after
+// issue, when the store reaches the head of the CU's memory queue.  An
+// instruction that overwrites one of those VGPRs before then stalls the
+// wave until the store drains -- under a saturated write stream that is
+// microseconds -- so a wave whose register allocator reuses a store's
+// VGPRs for the next store's address (or for the cost reduction) issues
+// its 13 stores one queue-drain at a time.  The same 6.8 GB memory path
+// ran 1.64 ms with that interleaving and 1.24 ms with the stores back to
+// back.  Here: the wave's cost is reduced first (cross-lane, no barrier),
+// the Jacobian is staged through LDS, and then every store is an inline-asm
+// global_store_dwordx4 whose operands stay live (so unclobbered) to the
+// end of the kernel.
+// ---------------------------------------------------------------------------
+
+typedef int cse_v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ cse_v4i AsV4i(double a, double b) {
+  const double2 v = make_double2(a, b);
+  cse_v4i d;
+  __builtin_memcpy(&d, &v, 16);
+  return d;
+}
+
+// 16-byte store at base + kOff bytes (kOff in [-4096, 4095]).  kPol: the
+// cache policy bits, 0 = nt sc1 (the default: streaming, not kept in the
+// XCD's L2; 6-8 % faster than nt alone on the evaluator's stream,
+// profiles/r02), 1 = none, 2 = sc1, 3 = sc0 sc1, 4 = nt, 5 = sc0 sc1 nt,
+// 6 = sc0 nt (tuning variants).
+template <int kOff, int kPol = 0>
+__device__ __forceinline__ void StoreNt16(double* base, const cse_v4i& d) {
+  static_assert(kOff >= -4096 && kOff <= 4095, "global offset out of range");
+  if constexpr (kPol == 4)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 nt" ::"v"(base), "v"(d), "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 1)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2" ::"v"(base), "v"(d), "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 2)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1" ::"v"(base), "v"(d), "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 3)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1" ::"v"(base), "v"(d),
+                 "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 0)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1 nt" ::"v"(base), "v"(d),
+                 "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 5)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1 nt" ::"v"(base), "v"(d),
+                 "i"(kOff)
+                 : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 nt" ::"v"(base), "v"(d),
+                 "i"(kOff)
+                 : "memory");
+}
+
+template <int kJ, int kCount, int kPol = 0>
+__device__ __forceinline__ void SegmentStoresFrom(double* b0, double* b1, const cse_v4i* q) {
+  if constexpr (kJ < kCount) {
+    StoreNt16<(kJ % 8) * 1024 - 4096, kPol>(kJ < 8 ? b0 : b1, q[kJ]);
+    SegmentStoresFrom<kJ + 1, kCount, kPol>(b0, b1, q);
+  }
+}
+
+// A wave's contiguous segment of kCount 16-byte pieces per lane: piece j
+// of lane l at seg + 16 * (64 j + l) bytes (1 KiB per instruction).
+template <int kCount>
+__device__ __forceinline__ void SegmentStores(double* seg, int lane, const cse_v4i* q,
+                                              double** keep0, double** keep1) {
+  static_assert(kCount <= 16, "segment too long");
+  double* b0 = seg + 2 * lane + 512;   // pieces 0..7 at offsets -4096..3072
+  double* b1 = seg + 2 * lane + 1536;  // pieces 8..15
+  SegmentStoresFrom<0, kCount>(b0, b1, q);
+  *keep0 = b0;
+  *keep1 = b1;
+}
+
+// A wave-uniform 64-bit value into SGPRs.
+__device__ __forceinline__ uint64_t WaveUniform64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Scalar (SMEM) stores of wave-uniform values; the caller issues
+// s_dcache_wb before the wave ends.
+__device__ __forceinline__ void ScalarStore64(uint64_t addr, uint64_t value) {
+  asm volatile("s_store_dwordx2 %0, %1, 0x0 glc" ::"s"(value), "s"(addr) : "memory");
+}
+__device__ __forceinline__ void ScalarStore32(uint64_t addr, uint32_t value) {
+  asm volatile("s_store_dword %0, %1, 0x0 glc" ::"s"(value), "s"(addr) : "memory");
+}
+
+template <int kCount>
+__device__ __forceinline__ void KeepAlive(const cse_v4i* q) {
+#pragma unroll
+  for (int j = 0; j < kCount; ++j) asm volatile("" ::"v"(q[j]));
+}
+
+// Can the wave take the back-to-back store tail?  Full chunk, 16-byte
+// pieces that tile every segment exactly, 16-byte-aligned destinations.
+template <class K, bool kJac, bool kCrs>
+__device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, N = Tr::N;
+  if (nw != kWave) return false;
+  if constexpr (NR % 2 != 0) return false;
+  if constexpr (kJac) {
+    if constexpr (kCrs) {
+      if ((NR * N) % 2 != 0) return false;
+    } else {
+      if ((NR * S0) % 2 != 0 || (NR * S1) % 2 != 0) return false;
+    }
+  }
+  uintptr_t m = 0;
+  if (a.residuals) m |= reinterpret_cast<uintptr_t>(a.residuals + a.res_base + (int64_t)NR * i0);
+  if (kJac && a.jacobian) {
+    if constexpr (kCrs) {
+      const int64_t row0 = a.jac_base[0][0] < a.jac_base[Tr::NB - 1][0] ? a.jac_base[0][0]
+                                                                         : a.jac_base[Tr::NB - 1][0];
+      m |= reinterpret_cast<uintptr_t>(a.jacobian + row0 + (int64_t)NR * N * i0);
+    } else {
+      m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0);
+      if constexpr (S1 > 0)
+        m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0);
+    }
+  }
+  return (m & 15) == 0;
+}
+
+// kTwoRound (BSM only): stage slot 0's cells, read them back, then slot
+// 1's into the same LDS (18 instead of 24 doubles per lane: 4 instead of 3
+// workgroups per CU).
+// kDebug (diagnostic variants, wrong results by design), bit flags: 1
+// replaces the functor by a trivial map of its inputs (memory-path floor),
+// 2 skips every output store (compute floor), 4 skips the LDS transpose
+// (each lane stores its own values at the coalesced positions).
+template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = false,
+          int kDebug = 0>
+__device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
+  constexpr int kOutLane = (kJac && (kDebug & 12) == 0)
+                              ? (kCrs ? NR * N
+                                      : kTwoRound ? (S0 > S1 ? NR * S0 : NR * S1)
+                                                  : NR * (S0 + S1))
+                              : 1;
+  constexpr int kCoopLane = kCoop >= 2 ? ((S0 + 1) & ~1) : kCoop == 1 ? S0 : 0;
+  constexpr int kStageLane = kCoopLane > kOutLane ? kCoopLane : kOutLane;
+  __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int64_t num_chunks = (a.n + kWave - 1) / kWave;
+  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (c >= num_chunks) {
+    if (lane == 0) a.partials[c] = 0.0;  // the group's partial slots are 4 per workgroup
+    return;
+  }
+  double* st = stage[wave];
+  const int64_t i0 = c * kWave;
+  const int64_t rem = a.n - i0;
+  const int nw = rem < kWave ? (int)rem : kWave;
+  const bool active = lane < nw;
+  const int64_t i = active ? i0 + lane : a.n - 1;
+
+  AffineInputs<K> in;
+  if constexpr (kCoop == 3) {
+    GatherCoopPacked<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
+  } else if constexpr (kCoop == 2) {
+    // Once-read streams (ids, observations, points) load non-temporally
+    // (-1.3 %, profiles/r02); kDebug bit 512 turns that off for A/B runs.
+    constexpr bool kNtLoads = (kDebug & 512) == 0;
+    int2 id;
+    if constexpr (kNtLoads && Tr::NB == 2) {
+      const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
+      id = make_int2((int)b, (int)(b >> 32));
+    } else {
+      id = LoadIds<K>(a, i);
+    }
+    GatherCoopDma<K, kNtLoads>(a, i, id, &in, st, lane);
+  } else if constexpr (kCoop == 1) {
+    GatherCoop<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
+  } else {
+    Gather<K>(a, i, LoadIds<K>(a, i), &in);
+  }
+  double r[NR], J0[NR * S0], J1[NR * S1p];
+  bool ok = true;
+  if constexpr ((kDebug & 1) != 0) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) r[k] = in.d[k % Tr::D] - in.x1[k % S1p];
+#pragma unroll
+    for (int q = 0; q < NR * S0; ++q) J0[q] = in.x0[q % S0] * in.d[0];
+#pragma unroll
+    for (int q = 0; q < NR * S1p; ++q) J1[q] = in.x1[q % S1p] * in.d[1 % Tr::D];
+  } else {
+    ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
+  }
+  if (ok && a.check_finite) {
+    bool bad = AnyNonFinite<NR>(r);
+    if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
+    ok = !bad;
+  }
+  double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+  if constexpr ((kDebug & 2) != 0) {
+#pragma unroll
+    for (int q = 0; q < NR * S0; ++q) cost += J0[q];
+#pragma unroll
+    for (int q = 0; q < NR * S1p; ++q) cost += J1[q];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) cost += r[k];
+  }
+  if (kJac && a.gradient != nullptr && active)
+    AddGradient<K>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0,
+                   S1 > 0 ? a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1 : nullptr, S0, S1,
+                   r, J0, J1);
+  // The wave's cost (fixed xor-butterfly order) and failure flag, before
+  // any store is queued.
+  double wsum = active ? cost : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
+  const bool failed = __ballot(active && !ok) != 0;
+  double* partial_dst = a.partials + c;
+  int* status_dst = a.status;
+
+  if constexpr ((kDebug & 2) != 0) {
+    if (lane == 0) *partial_dst = wsum;
+    return;
+  }
+  if (!FastTail<K, kJac, kCrs>(a, i0, nw)) {
+    if constexpr ((kDebug & 12) == 0)
+      StageAndStore<K, kJac, kCrs, true, !kTwoRound>(a, st, lane, active, i0, nw, r, J0, J1);
+    if (lane == 0) {
+      *partial_dst = wsum;
+      if (failed) *status_dst = 1;
+    }
+    return;
+  }
+
+  // Stage the Jacobian, read it back as 16-byte pieces in segment order.
+  constexpr int kQ0 = kJac ? (kCrs ? NR * N / 2 : NR * S0 / 2) : 0;  // pieces per lane, seg 0
+  constexpr int kQ1 = (kJac && !kCrs && S1 > 0) ? NR * S1 / 2 : 0;   // seg 1 (E cells)
+  const bool jac = kJac && a.jacobian != nullptr;
+  cse_v4i q0[kQ0 > 0 ? kQ0 : 1], q1[kQ1 > 0 ? kQ1 : 1];
+  double* seg0 = nullptr;
+  double* seg1 = nullptr;
+  if constexpr (kJac && (kDebug & 8) != 0 && !kCrs) {
+    // Diagnostic: one register quad (the wave's cost) for every store.
+    if (jac) {
+      const cse_v4i one = AsV4i(wsum, wsum);
+#pragma unroll
+      for (int j = 0; j < kQ0; ++j) q0[j] = one;
+#pragma unroll
+      for (int j = 0; j < kQ1; ++j) q1[j] = one;
+      seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+      seg1 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+    }
+  } else if constexpr (kJac && (kDebug & 4) != 0 && !kCrs) {
+    if (jac) {
+#pragma unroll
+      for (int j = 0; j < kQ0; ++j) q0[j] = AsV4i(J0[2 * j], J0[2 * j + 1]);
+#pragma unroll
+      for (int j = 0; j < kQ1; ++j) q1[j] = AsV4i(J1[2 * j], J1[2 * j + 1]);
+      seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+      seg1 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+    }
+  } else if constexpr (kJac) {
+    if (jac) {
+      if constexpr (kCrs) {
+        const int64_t row0 = a.jac_base[0][0] < a.jac_base[Tr::NB - 1][0]
+                                 ? a.jac_base[0][0]
+                                 : a.jac_base[Tr::NB - 1][0];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          const int c0 = (int)(a.jac_base[0][k] - row0);
+#pragma unroll
+          for (int cc = 0; cc < S0; ++cc) st[lane * NR * N + c0 + cc] = J0[k * S0 + cc];
+          if constexpr (S1 > 0) {
+            const int c1 = (int)(a.jac_base[1][k] - row0);
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) st[lane * NR * N + c1 + cc] = J1[k * S1p + cc];
+          }
+        }
+        seg0 = a.jacobian + row0 + (int64_t)NR * N * i0;
+      } else if constexpr (kTwoRound) {
+#pragma unroll
+        for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
+        seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < kQ0; ++j) {
+          const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
+          q0[j] = AsV4i(v.x, v.y);
+        }
+        if constexpr (S1 > 0) {
+          // Every lane's reads of round 1 must land before round 2 writes.
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+          seg1 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+        }
+      } else {
+        double* st1 = st + kWave * NR * S0;
+#pragma unroll
+        for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
+        if constexpr (S1 > 0) {
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) st1[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+          seg1 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+        }
+        seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if constexpr (kCrs || !kTwoRound) {
+#pragma unroll
+        for (int j = 0; j < kQ0; ++j) {
+          const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
+          q0[j] = AsV4i(v.x, v.y);
+        }
+      }
+      if constexpr (kQ1 > 0) {
+        const double* st1 = kTwoRound ? st : st + kWave * NR * S0;
+#pragma unroll
+        for (int j = 0; j < kQ1; ++j) {
+          const double2 v = reinterpret_cast<const double2*>(st1)[j * kWave + lane];
+          q1[j] = AsV4i(v.x, v.y);
+        }
+      }
+    }
+  }
+  // Residual pieces: the lane's own NR doubles (NR even).
+  constexpr int kQr = NR / 2;
+  cse_v4i qr[kQr];
+#pragma unroll
+  for (int k = 0; k < kQr; ++k) qr[k] = AsV4i(r[2 * k], r[2 * k + 1]);
+  double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;
+
+  // Every address and the wave's scalar outputs are computed (and pinned by
+  // the empty asm) before the first store: after it the wave runs only
+  // stores and SALU, so nothing waits on the store queue.
+  double *f0 = nullptr, *f1 = nullptr, *e0 = nullptr, *e1 = nullptr;
+  if (jac) {
+    f0 = seg0 + 2 * lane + 512;
+    f1 = seg0 + 2 * lane + 1536;
+    if constexpr (kQ1 > 0) {
+      e0 = seg1 + 2 * lane + 512;
+      e1 = seg1 + 2 * lane + 1536;
+    }
+  }
+  const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(partial_dst));
+  const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, wsum));
+  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
+
+  // ---- every store of the wave, back to back ----
+  constexpr int kPol = (kDebug >> 4) & 15;  // tuning variants only; 0 = nt sc1
+  if (jac) {
+    SegmentStoresFrom<0, kQ0, kPol>(f0, f1, q0);
+    if constexpr (kQ1 > 0) SegmentStoresFrom<0, kQ1, kPol>(e0, e1, q1);
+  }
+  if (a.residuals) {  // a kernel argument: a scalar branch, no VALU after the stores
+    if constexpr (kQr >= 1) StoreNt16<0, kPol>(rdst, qr[0]);
+    if constexpr (kQr >= 2) StoreNt16<16, kPol>(rdst, qr[1]);
+    if constexpr (kQr >= 3) StoreNt16<32, kPol>(rdst, qr[2]);
+  }
+  // The cost partial (and the failure flag) by scalar stores: a one-lane
+  // vector store here costs ~10 % of the kernel (tools/membench2.hip, m2).
+  ScalarStore64(s_partial, s_wsum);
+  if (failed) ScalarStore32(WaveUniform64(reinterpret_cast<uint64_t>(status_dst)), 1u);
+  asm volatile("s_dcache_wb" ::: "memory");
+  KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
+  KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
+  KeepAlive<kQr>(qr);
+  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
+}
+
+// Diagnostic only: tools/membench2.hip's m1 memory path (camera gather
+// from the packed table, 13 stores of one register quad) on the
+// evaluator's real buffers (BSM, Snavely shapes).  Wrong results by design.
+// kStep walks it towards EvaluateAffineChunks one change at a time:
+//   0 m1 as in membench (register gather, compiler stores, lane-0 partial)
+//   1 + the shipped tail (asm stores at SegmentStoresFrom bases, scalar partial)
+//   2 + LDS-DMA camera gather (GatherCoopDma)
+//   3 + distinct data per store (q[j] = v * j)
+template <int kStep>
+__global__ __launch_bounds__(kBlockThreads) void MembenchM1Kernel(const GroupArgs a) {
+  __shared__ double lds[kWavesPerBlock][kWave * 10];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x / 64;
+  const int64_t chunks = (a.n + 63) / 64;
+  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (c >= chunks) return;
+  int64_t i = c * 64 + lane;
+  if (i >= a.n) i = a.n - 1;
+  double v;
+  if constexpr (kStep >= 2) {
+    AffineInputs<SnavelyKind> in;
+    GatherCoopDma<SnavelyKind>(a, i, LoadIds<SnavelyKind>(a, i), &in, lds[wave], lane);
+    v = in.d[0] + in.d[1] + in.x1[0] + in.x1[1] + in.x1[2];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v += in.x0[k];
+  } else {
+    const int2 id = *reinterpret_cast<const int2*>(a.ids + 2 * i);
+    const double2 o = reinterpret_cast<const double2*>(a.data)[i];
+    const double* pt = a.state + a.state_base[1] + 3L * id.y;
+    v = o.x + o.y + pt[0] + pt[1] + pt[2];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int p = k * 64 + lane;
+      const int t = p / 5, q = p % 5;
+      const int cid = __shfl(id.x - a.packed0_lo, t, 64);
+      const double2 w = *reinterpret_cast<const double2*>(a.packed0 + 10L * cid + 2 * q);
+      *reinterpret_cast<double2*>(lds[wave] + t * 10 + 2 * q) = w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s += lds[wave][lane * 10 + k];
+    __builtin_amdgcn_wave_barrier();
+    v += s;
+  }
+  double* res = a.residuals + a.res_base;
+  double* E = a.jacobian + a.jac_base[1][0];
+  double* F = a.jacobian + a.jac_base[0][0];
+  if constexpr (kStep == 0) {
+    __builtin_nontemporal_store(v, res + 128 * c + 2 * lane);
+    __builtin_nontemporal_store(v, res + 128 * c + 2 * lane + 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      __builtin_nontemporal_store(v, E + 384 * c + 128 * k + 2 * lane);
+      __builtin_nontemporal_store(v, E + 384 * c + 128 * k + 2 * lane + 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      __builtin_nontemporal_store(v, F + 1152 * c + 128 * k + 2 * lane);
+      __builtin_nontemporal_store(v, F + 1152 * c + 128 * k + 2 * lane + 1);
+    }
+    if (lane == 0) a.partials[c] = 0.0;
+  } else {
+    cse_v4i q0[9], q1[3];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) q0[j] = kStep >= 3 ? AsV4i(v * j, v * (j + 1)) : AsV4i(v, v);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) q1[j] = kStep >= 3 ? AsV4i(v * (j + 9), v * j) : AsV4i(v, v);
+    const cse_v4i qr = AsV4i(v, v);
+    double* seg0 = F + 1152 * c;
+    double* seg1 = E + 384 * c;
+    double* rdst = res + 128 * c + 2 * lane;
+    double* f0 = seg0 + 2 * lane + 512;
+    double* f1 = seg0 + 2 * lane + 1536;
+    double* e0 = seg1 + 2 * lane + 512;
+    double* e1 = seg1 + 2 * lane + 1536;
+    const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(a.partials + c));
+    const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, v));
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
+    SegmentStoresFrom<0, 9>(f0, f1, q0);
+    SegmentStoresFrom<0, 3>(e0, e1, q1);
+    StoreNt16<0>(rdst, qr);
+    ScalarStore64(s_partial, 0);
+    asm volatile("s_dcache_wb" ::: "memory");
+    KeepAlive<9>(q0);
+    KeepAlive<3>(q1);
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(qr));
+  }
+}
+
+template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = false,
+          int kDebug = 0>
+__global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug>(a);
+}
+
 // The general (table) path; also runs affine groups when
 // force_general_layout is set.  One block per lane, one launch-wide grid.
 template <class K, int kLoss, bool kJac>
 __global__ __launch_bounds__(kBlockThreads) void EvaluateGroupKernel(const GroupArgs a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
-  __shared__ double lds_sum[kWavesPerBlock];
 
   const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
   const bool active = i < a.n;
@@ -773,8 +1302,13 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateGroupKernel(const Group
       }
     }
   }
-  const double t = WorkgroupSum(cost, lds_sum);
-  if (threadIdx.x == 0) a.partials[blockIdx.x] = t;
+  // One partial per wave (the wave's 64 blocks are the affine kernels'
+  // chunk, so both paths sum the same partials in the same order).
+  double w = cost;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    a.partials[(int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave] = w;
 }
 
 // First pass of the cost reduction when there are many partials: workgroup
