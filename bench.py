@@ -228,7 +228,7 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "kernel_ms_avg": kernel_ms,
                 "kernel_ms_avg_max_rank": kernel_ms_max,
-                "kernel": "cse::EvaluateAffinePersistentD<SnavelyKind, loss, jacobian, layout, ...>",
+                "kernel": "cse::EvaluateAffineChunks<SnavelyKind, loss, jacobian, layout, ...>",
                 "traffic_source": "profiles/pmc_<config>_<loss>_<format>.json (rocprofv3 FETCH_SIZE/WRITE_SIZE)",
             },
             "cpu_baseline": cpu,
