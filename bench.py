@@ -55,6 +55,10 @@ def parse():
                     help="0 = the whole workload (about 1 s per eval on 16 cores)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
+    ap.add_argument("--host-copy", action="store_true",
+                    help="also time evaluations that copy the rank's residuals and Jacobian "
+                         "strips to pinned host memory (the reference's D2H seam; reported "
+                         "under 'host_copy', never as value)")
     return ap.parse_args()
 
 
@@ -122,17 +126,25 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # One process per GPU.  (Ranks beyond the visible devices share them:
+    # that only happens in a 1-GPU rehearsal of the multi-rank path, which
+    # also sets CSE_DIST_BACKEND=gloo since RCCL needs distinct devices.)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    backend = os.environ.get("CSE_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     t_build = time.perf_counter()
     prog, shard_info = build_shard(args, rank, world)
     build_s = time.perf_counter() - t_build
 
     stream = torch.cuda.current_stream(dev)
-    ev = ca.Evaluator(prog, device=local_rank, profile=True, stream=stream.cuda_stream)
+    ev = ca.Evaluator(prog, device=dev_index, profile=True, stream=stream.cuda_stream)
     info = ev.info()
     f64 = torch.float64
     state = torch.from_numpy(prog.state).to(dev)
@@ -178,7 +190,46 @@ def main():
     if status != 0:
         raise SystemExit(f"evaluation failed (status {status})")
 
-    bytes_per_launch = info.bytes_jacobian_eval
+    host_copy = None
+    if args.host_copy:
+        # The reference's seam: outputs handed back in host memory.  Each rank
+        # copies its contiguous residual and Jacobian strips (shard.Shard) to
+        # pinned buffers on the evaluator's stream.
+        hres = torch.empty(prog.num_residuals, dtype=f64, pin_memory=True)
+        hjac = torch.empty(prog.num_jacobian_values, dtype=f64, pin_memory=True)
+
+        def step_host():
+            step()
+            hres.copy_(res, non_blocking=True)
+            hjac.copy_(jac, non_blocking=True)
+
+        step_host()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        th = time.perf_counter()
+        for _ in range(args.steps):
+            step_host()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        eh = time.perf_counter() - th
+        if world > 1:
+            t = torch.tensor([eh], dtype=f64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            eh = float(t[0])
+        d2h = (prog.num_residuals + prog.num_jacobian_values) * 8
+        host_copy = {
+            "value": (world if (args.scaling == "weak" or world == 1) else 1) * args.steps / eh,
+            "unit": "evals/s", "ms_per_step": eh / args.steps * 1e3,
+            "d2h_bytes_per_rank": d2h, "d2h_GBps_per_rank": d2h * args.steps / eh / 1e9,
+            "what": "device evaluation + D2H of the rank's residual and Jacobian strips into "
+                    "pinned host memory, every step (PCIe-inclusive; not the headline value)"}
+
+    # Compulsory bytes (SURVEY.md §8 d); the gradient adds its 8 B per
+    # effective parameter written.
+    bytes_per_launch = info.bytes_jacobian_eval + (8 * prog.num_effective_parameters
+                                                   if args.gradient else 0)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     weak = args.scaling == "weak" or world == 1
     value = (world if weak else 1) * args.steps / elapsed
@@ -232,6 +283,7 @@ def main():
                 "traffic_source": "profiles/pmc_<config>_<loss>_<format>.json (rocprofv3 FETCH_SIZE/WRITE_SIZE)",
             },
             "cpu_baseline": cpu,
+            "host_copy": host_copy,
             "speedup_vs_cpu": (value / world / cpu["value"]) if cpu else None,
             "build_s": build_s,
             "reference_published": {"value": 0.6455, "unit": "evals/s",

@@ -99,6 +99,19 @@ struct Group {
   int64_t slot0_count = 0;
   int slot0_stride = 0;
   DevBuf<double> packed0;
+  // Gradient post-pass plan per slot (affine groups with a Jacobian layout).
+  struct GradPlan {
+    bool ready = false;
+    bool wave = false;  // one wave (not one lane) per parameter block
+    int32_t lo = 0;
+    int64_t count = 0;
+    DevBuf<int32_t> perm;  // empty = identity
+    DevBuf<int64_t> off;
+    // wave mode: chunks of at most cse::kGradChunk blocks
+    DevBuf<int64_t> chunk_begin, chunk_off;
+    DevBuf<double> chunk_partial;
+    int64_t nchunks = 0;
+  } grad[2];
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -339,6 +352,96 @@ int Validate(const cse_problem_desc* d) {
 
 // Is the group table-free?  Returns the Policy (see evaluate_kernel.hpp
 // for the two affine shapes).
+// Blocks of slot j listed per parameter block (stable counting sort): the
+// gradient post-pass sums each parameter block's blocks in this order.
+int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group::GradPlan* plan,
+                  hipStream_t s) {
+  const int64_t n = g.num_blocks;
+  int32_t lo = g.parameter_block_ids[j], hi = lo;
+  for (int64_t i = 0; i < n; ++i) {
+    lo = std::min(lo, g.parameter_block_ids[i * k.nb + j]);
+    hi = std::max(hi, g.parameter_block_ids[i * k.nb + j]);
+  }
+  const int64_t count = (int64_t)hi - lo + 1;
+  std::vector<int64_t> off(count + 1, 0);
+  bool sorted = true;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t id = g.parameter_block_ids[i * k.nb + j];
+    ++off[id - lo + 1];
+    if (i > 0 && id < g.parameter_block_ids[(i - 1) * k.nb + j]) sorted = false;
+  }
+  for (int64_t p = 0; p < count; ++p) off[p + 1] += off[p];
+  int rc;
+  if (!sorted) {
+    std::vector<int32_t> perm(n);
+    std::vector<int64_t> next(off.begin(), off.end() - 1);
+    for (int64_t i = 0; i < n; ++i) perm[next[g.parameter_block_ids[i * k.nb + j] - lo]++] = (int32_t)i;
+    if ((rc = plan->perm.upload(perm.data(), perm.size(), s))) return rc;
+    if (hipStreamSynchronize(s) != hipSuccess) return Fail(CSE_ERR_HIP, "hipStreamSynchronize failed");
+  }
+  if ((rc = plan->off.upload(off.data(), off.size(), s))) return rc;
+  if (hipStreamSynchronize(s) != hipSuccess) return Fail(CSE_ERR_HIP, "hipStreamSynchronize failed");
+  plan->lo = lo;
+  plan->count = count;
+  plan->wave = !sorted && n >= 32 * count;  // on average 32+ blocks per parameter block
+  if (plan->wave) {
+    std::vector<int64_t> begin, coff(count + 1, 0);
+    for (int64_t p = 0; p < count; ++p) {
+      coff[p] = (int64_t)begin.size();
+      for (int64_t q = off[p]; q < off[p + 1]; q += cse::kGradChunk) begin.push_back(q);
+    }
+    coff[count] = (int64_t)begin.size();
+    plan->nchunks = (int64_t)begin.size();
+    // Chunk c covers [begin[c], begin[c + 1]): a parameter block's last
+    // chunk ends at off[p + 1], where the next non-empty one starts.
+    begin.push_back(n);
+    if ((rc = plan->chunk_begin.upload(begin.data(), begin.size(), s))) return rc;
+    if ((rc = plan->chunk_off.upload(coff.data(), coff.size(), s))) return rc;
+    const int size = j == 0 ? k.s0 : k.s1;
+    if ((rc = plan->chunk_partial.alloc((size_t)std::max<int64_t>(1, plan->nchunks) * size)))
+      return rc;
+    if (hipStreamSynchronize(s) != hipSuccess) return Fail(CSE_ERR_HIP, "hipStreamSynchronize failed");
+  }
+  plan->ready = true;
+  return CSE_OK;
+}
+
+template <int NR, int S>
+void LaunchGradSlot(const cse::GradArgs& ga, const Group::GradPlan& P, hipStream_t s) {
+  if (ga.perm == nullptr) {  // identity order: contiguous block ranges (points)
+    hipLaunchKernelGGL((cse::GradientRangeKernel<NR, S>),
+                       dim3((unsigned)((ga.count + cse::kWave - 1) / cse::kWave)), dim3(cse::kWave),
+                       0, s, ga);
+  } else if (P.wave) {  // many blocks per parameter block (cameras): chunks
+    const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
+    const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
+    if (P.nchunks > 0)
+      hipLaunchKernelGGL((cse::GradientLanesKernel<NR, S>), grid, dim3(cse::kBlockThreads), 0, s,
+                         ga, ch);
+    hipLaunchKernelGGL((cse::GradientChunkReduceKernel<S>),
+                       dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                       dim3(cse::kBlockThreads), 0, s, ga, ch);
+  } else {
+    hipLaunchKernelGGL((cse::GradientSlotKernel<NR, S, false>),
+                       dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                       dim3(cse::kBlockThreads), 0, s, ga);
+  }
+}
+
+bool GradSupported(int nr, int size) {
+  return (nr == 2 && (size == 9 || size == 3 || size == 7 || size == 10)) || (nr == 3 && size == 3);
+}
+
+bool LaunchGradPass(int nr, int size, const cse::GradArgs& ga, const Group::GradPlan& P,
+                    hipStream_t s) {
+  if (nr == 2 && size == 9) return LaunchGradSlot<2, 9>(ga, P, s), true;
+  if (nr == 2 && size == 3) return LaunchGradSlot<2, 3>(ga, P, s), true;
+  if (nr == 2 && size == 7) return LaunchGradSlot<2, 7>(ga, P, s), true;
+  if (nr == 2 && size == 10) return LaunchGradSlot<2, 10>(ga, P, s), true;
+  if (nr == 3 && size == 3) return LaunchGradSlot<3, 3>(ga, P, s), true;
+  return false;
+}
+
 int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const KindShape& k,
                   Group* G) {
   const int64_t n = g.num_blocks;
@@ -502,7 +605,12 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     const bool dma = G.packed0.p != nullptr;
     LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma);
     if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
-    const cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, d_grad);
+    // Gradient: a deterministic post-pass over the written residuals and
+    // Jacobian when the group has plans for all its slots, else in-kernel
+    // FP64 atomics (as the reference).
+    bool grad_pass = d_grad && d_res && d_jac && G.affine;
+    for (int j = 0; j < G.shape.nb; ++j) grad_pass = grad_pass && G.grad[j].ready;
+    const cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
       const int64_t total = G.slot0_count * G.slot0_stride;
@@ -512,6 +620,27 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
+    if (grad_pass) {
+      const int sizes[2] = {G.shape.s0, G.shape.s1};
+      for (int j = 0; j < G.shape.nb; ++j) {
+        const Group::GradPlan& P = G.grad[j];
+        cse::GradArgs ga{};
+        ga.jac = d_jac;
+        for (int r = 0; r < G.shape.nr && r < 3; ++r) ga.jrow[r] = G.jac_base[j][r];
+        ga.jstride = G.jac_stride[j];
+        ga.res = d_res;
+        ga.res_base = G.res_base;
+        ga.perm = P.perm.p;
+        ga.off = P.off.p;
+        ga.count = P.count;
+        ga.lo = P.lo;
+        ga.grad = d_grad;
+        ga.delta_base = G.delta_base[j];
+        if (!LaunchGradPass(G.shape.nr, sizes[j], ga, P, ev->stream))
+          return Fail(CSE_ERR_UNSUPPORTED, "no gradient pass for this shape");
+        CSE_HIP(hipGetLastError());
+      }
+    }
   }
   if (timing.first) {
     if (ev->groups.empty()) CSE_HIP(hipEventRecord(timing.first, ev->stream));
@@ -674,6 +803,12 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
         getenv("CSE_NO_DMA_GATHER") == nullptr &&
         (rc = G.packed0.alloc((size_t)G.slot0_count * G.slot0_stride)))
       return bail(rc);
+    if (G.affine && ev->has_layout && getenv("CSE_ATOMIC_GRADIENT") == nullptr) {
+      const int sizes[2] = {k.s0, k.s1};
+      for (int j = 0; j < k.nb; ++j)
+        if (GradSupported(k.nr, sizes[j]) && (rc = BuildGradPlan(g, k, j, &G.grad[j], s)))
+          return bail(rc);
+    }
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
     if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
     if (!G.affine && g.residual_block_index &&

@@ -1311,6 +1311,197 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateGroupKernel(const Group
     a.partials[(int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave] = w;
 }
 
+// ---------------------------------------------------------------------------
+// Gradient g = J^T r as a deterministic post-pass over the outputs just
+// written (affine groups with residuals and Jacobian requested).  The
+// reference adds J^T r with per-element FP64 atomics inside the evaluate
+// kernel (cuda_evaluator_kernel.h:149-160); with ~2,100 observations per
+// camera and 64 random addresses per wave instruction those atomics ran at
+// 18 ms per evaluation here (0.05 of the HBM roofline).  Instead, for each
+// slot, the blocks are listed per parameter block (counting sort at create
+// time; identity for the points of a Schur-ordered problem) and every
+// parameter block sums its blocks' J_b^T r_b in a fixed order:
+//   kWaveMode = false: one lane per parameter block (few blocks each:
+//                      points), true: one wave per parameter block (many
+//                      blocks each: cameras), lanes strided over the blocks
+//                      and a fixed xor-butterfly.
+// ---------------------------------------------------------------------------
+struct GradArgs {
+  const double* jac;
+  int64_t jrow[3];   // start of row k of the slot's cell for block 0
+  int64_t jstride;   // per block
+  const double* res;
+  int64_t res_base;
+  const int32_t* perm;  // blocks sorted by parameter block; null = identity
+  const int64_t* off;   // [count + 1]
+  int64_t count;        // parameter blocks lo .. lo + count - 1
+  int32_t lo;
+  double* grad;
+  int64_t delta_base;   // delta offset of id = delta_base + S * id
+};
+
+template <int NR, int S, bool kWaveMode>
+__global__ __launch_bounds__(kBlockThreads) void GradientSlotKernel(const GradArgs g) {
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  int64_t p;
+  int64_t q0, q1, qs;
+  if constexpr (kWaveMode) {
+    p = ((int64_t)blockIdx.x * kBlockThreads + threadIdx.x) / kWave;
+    if (p >= g.count) return;
+    q0 = g.off[p] + (threadIdx.x & (kWave - 1));
+    q1 = g.off[p + 1];
+    qs = kWave;
+  } else {
+    p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+    if (p >= g.count) return;
+    q0 = g.off[p];
+    q1 = g.off[p + 1];
+    qs = 1;
+  }
+  for (int64_t q = q0; q < q1; q += qs) {
+    const int64_t b = g.perm ? (int64_t)g.perm[q] : q;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double rk = g.res[g.res_base + (int64_t)NR * b + k];
+      const double* row = g.jac + g.jrow[k] + g.jstride * b;
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[c] += row[c] * rk;
+    }
+  }
+  double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+  if constexpr (kWaveMode) {
+#pragma unroll
+    for (int c = 0; c < S; ++c)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) dst[c] += acc[c];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < S; ++c) dst[c] += acc[c];
+  }
+}
+
+// Parameter blocks with many blocks (cameras): their block lists are cut
+// into chunks of at most kGradChunk blocks, one wave per chunk
+// (GradientLanesKernel), and GradientChunkReduceKernel adds each parameter
+// block's chunk partials in order.  Deterministic, no atomics.  (An
+// element-per-lane variant that reads whole cells per instruction measured
+// 3-10 % slower: the random cells and residual pairs cost whole lines
+// either way.)
+constexpr int kGradChunk = 512;
+
+struct GradChunks {
+  const int64_t* begin;      // [nchunks + 1] chunk c covers perm[begin[c], begin[c+1])
+  const int64_t* chunk_off;  // [count + 1] chunks of parameter block p
+  double* partial;           // [nchunks][S]
+  int64_t nchunks;
+};
+
+// Lane per block: each lane reads its blocks' whole cells
+// (rows of S contiguous doubles) and residual pairs; S accumulators per
+// lane, combined by a fixed xor-butterfly.
+template <int NR, int S>
+__global__ __launch_bounds__(kBlockThreads) void GradientLanesKernel(const GradArgs g,
+                                                                     const GradChunks ch) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (cid >= ch.nchunks) return;
+  const int64_t q1 = ch.begin[cid + 1];
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
+    const int64_t b = g.perm ? (int64_t)g.perm[q] : q;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double rk = g.res[g.res_base + (int64_t)NR * b + k];
+      const double* row = g.jac + g.jrow[k] + g.jstride * b;
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[c] += row[c] * rk;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < S; ++c)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < S; ++c) ch.partial[cid * S + c] = acc[c];
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const GradArgs g,
+                                                                           const GradChunks ch) {
+  const int64_t p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (p >= g.count) return;
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q)
+#pragma unroll
+    for (int c = 0; c < S; ++c) acc[c] += ch.partial[q * S + c];
+  double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+#pragma unroll
+  for (int c = 0; c < S; ++c) dst[c] += acc[c];
+}
+
+// Identity order (the points of a Schur-ordered problem): one 64-thread
+// workgroup per 64 consecutive parameter blocks, whose blocks form one
+// contiguous range.  The range is walked in tiles of 64 blocks: all lanes
+// form the products J[e] * r[k] element by element (contiguous loads), park
+// them in LDS, and then thread t sums parameter block t's blocks of the
+// tile in block, row order.
+template <int NR, int S>
+__global__ __launch_bounds__(kWave) void GradientRangeKernel(const GradArgs g) {
+  constexpr int E = NR * S;
+  constexpr int T = kWave;  // blocks per tile
+  __shared__ double prod[T * E];
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kWave;
+  const int64_t p = p0 + lane;
+  const int64_t pend = p0 + kWave < g.count ? p0 + kWave : g.count;
+  const int64_t B0 = g.off[p0], B1 = g.off[pend];
+  const int64_t my0 = p < g.count ? g.off[p] : B1, my1 = p < g.count ? g.off[p + 1] : B1;
+  double acc[S];
+#pragma unroll
+  for (int cc = 0; cc < S; ++cc) acc[cc] = 0.0;
+  for (int64_t t0 = B0; t0 < B1; t0 += T) {
+    const int nb = B1 - t0 < T ? (int)(B1 - t0) : T;
+#pragma unroll
+    for (int it = 0; it < E; ++it) {
+      const int t = it * kWave + lane;  // element t of the tile
+      const int bm = t / E, e = t - bm * E, k = e / S, cc = e - k * S;
+      double v = 0.0;
+      if (bm < nb) {
+        const int64_t b = t0 + bm;
+        v = g.jac[g.jrow[k] + g.jstride * b + cc] * g.res[g.res_base + (int64_t)NR * b + k];
+      }
+      prod[t] = v;
+    }
+    __syncthreads();
+    const int64_t lo = my0 > t0 ? my0 : t0, hi = my1 < t0 + nb ? my1 : t0 + nb;
+    for (int64_t b = lo; b < hi; ++b) {
+      const int bm = (int)(b - t0);
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+#pragma unroll
+        for (int cc = 0; cc < S; ++cc) acc[cc] += prod[bm * E + k * S + cc];
+    }
+    __syncthreads();
+  }
+  if (p < g.count) {
+    double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+#pragma unroll
+    for (int cc = 0; cc < S; ++cc) dst[cc] += acc[cc];
+  }
+}
+
 // First pass of the cost reduction when there are many partials: workgroup
 // b sums partials [b*per, (b+1)*per) in a fixed order.
 __global__ __launch_bounds__(kBlockThreads) void PartialSumKernel(const double* partials,
