@@ -281,3 +281,19 @@ def test_problem_13682_full_size(gpu):
     assert info.num_affine_groups == 1
     ref = oracle_eval(prog, threads=16, residuals=True, gradient=False, jacobian=True)
     assert_parity(got, ref, "problem-13682")
+
+
+def test_gradient_post_pass_deterministic_and_matches_atomics(gpu):
+    # Affine groups sum J^T r per parameter block in a fixed order (no
+    # atomics): bit-identical run to run, and equal (to the tolerance) to the
+    # in-kernel atomic path that serves gradient-without-Jacobian requests.
+    prog = small_bal(C=24, P=3000, O_=20000, loss=ca.Loss.huber(1.0))
+    ref = oracle_eval(prog)
+    ev = ca.Evaluator(prog)
+    a = ev.evaluate()
+    b = ev.evaluate()
+    atomic = ev.evaluate(residuals=False, gradient=True, jacobian=False)
+    ev.close()
+    assert_parity(a, ref)
+    assert np.array_equal(a[3], b[3])
+    assert is_approx(atomic[3], a[3], 1e-13)
