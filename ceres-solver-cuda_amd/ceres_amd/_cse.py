@@ -107,6 +107,8 @@ SIGNATURES = {
                                       C.c_void_p, C.c_void_p]),
     "cse_wait": (C.c_int, [C.c_void_p]),
     "cse_set_plus_jacobians": (C.c_int, [C.c_void_p, P_f64]),
+    "cse_plus_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_plus": (C.c_int, [C.c_void_p, P_f64, P_f64, P_f64]),
     "cse_destroy": (None, [C.c_void_p]),
     "cse_last_error": (C.c_char_p, []),
     "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),

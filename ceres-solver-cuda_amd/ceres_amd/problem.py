@@ -402,6 +402,20 @@ class Evaluator:
     def wait(self):
         return _cse.check(_cse.lib().cse_wait(self.handle), "cse_wait")
 
+    def plus(self, state, delta):
+        """Evaluator::Plus (program.cc:121-149) on the GPU, host arrays."""
+        state = np.ascontiguousarray(state, np.float64)
+        delta = np.ascontiguousarray(delta, np.float64)
+        out = np.empty_like(state)
+        _cse.check(_cse.lib().cse_plus(self.handle, _ptr(state, C.c_double),
+                                       _ptr(delta, C.c_double), _ptr(out, C.c_double)), "cse_plus")
+        return out
+
+    def plus_device(self, d_state, d_delta, d_out):
+        """Device-pointer Plus on the evaluator's stream.  Async."""
+        return _cse.check(_cse.lib().cse_plus_device(self.handle, d_state, d_delta, d_out),
+                          "cse_plus_device")
+
     def kernel_stats(self):
         last, total, n = C.c_double(), C.c_double(), C.c_int64()
         _cse.check(_cse.lib().cse_kernel_stats(self.handle, C.byref(last), C.byref(total),

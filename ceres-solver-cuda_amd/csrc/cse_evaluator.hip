@@ -61,6 +61,12 @@ struct DevBuf {
     n = count;
     return CSE_OK;
   }
+  // Allocate on first use / grow; keeps the buffer when large enough.
+  int ensure(size_t count) {
+    if (p && n >= count) return CSE_OK;
+    release();
+    return alloc(count);
+  }
   int upload(const T* h, size_t count, hipStream_t s) {
     int rc = alloc(count);
     if (rc) return rc;
@@ -303,6 +309,11 @@ struct cse_evaluator {
   DevBuf<double> cstate, plus_jac;
   DevBuf<int64_t> res_layout, jac_layout, jac_offsets;
   DevBuf<double> partials, partials2;
+  // Program::Plus (cse_plus_device): runs of manifold-free state entries.
+  bool plus_supported = true;
+  std::vector<cse::PlusRun> plus_runs_host;
+  DevBuf<cse::PlusRun> plus_runs;
+  DevBuf<double> h_delta, h_plus;
   DevBuf<int> status;  // [0] running flag, [1] last status
   // Host-path buffers (allocated on first use).
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
@@ -719,6 +730,28 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   ev->num_jacobian_values = d->num_jacobian_values;
   ev->num_plus_jacobian_values = d->num_plus_jacobian_values;
   ev->has_layout = d->jacobian_per_residual_layout && d->jacobian_per_residual_offsets;
+  {
+    // Plus runs: active blocks sorted by state offset, merged while
+    // contiguous with a constant delta shift.
+    std::vector<std::pair<int64_t, int64_t>> blocks;  // (state_offset, index)
+    for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
+      const cse_parameter_block& pb = d->parameter_blocks[b];
+      if (pb.is_constant) continue;
+      if (pb.plus_jacobian_offset >= 0 || pb.tangent_size != pb.size) ev->plus_supported = false;
+      blocks.emplace_back(pb.state_offset, b);
+    }
+    std::sort(blocks.begin(), blocks.end());
+    for (const auto& e : blocks) {
+      const cse_parameter_block& pb = d->parameter_blocks[e.second];
+      const int64_t shift = pb.state_offset - pb.delta_offset;
+      auto& R = ev->plus_runs_host;
+      if (!R.empty() && R.back().state_begin + R.back().length == pb.state_offset &&
+          R.back().delta_shift == shift)
+        R.back().length += pb.size;
+      else
+        R.push_back({pb.state_offset, pb.size, shift});
+    }
+  }
 
   // Groups.
   int64_t covered_res = 0, covered_jac = 0;
@@ -919,6 +952,51 @@ int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians) {
   return CSE_OK;
 }
 
+int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_delta,
+                    double* d_state_plus_delta) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (!ev->plus_supported)
+    return Fail(CSE_ERR_UNSUPPORTED, "Plus on device: an active parameter block has a manifold");
+  if (ev->plus_runs_host.empty()) return CSE_OK;
+  if (!d_state || !d_delta || !d_state_plus_delta) return Fail(CSE_ERR_INVALID, "null pointer");
+  CSE_HIP(hipSetDevice(ev->device));
+  if (!ev->plus_runs.p) {
+    int rc = ev->plus_runs.upload(ev->plus_runs_host.data(), ev->plus_runs_host.size(), ev->stream);
+    if (rc) return rc;
+  }
+  const int64_t n = ev->num_parameters;
+  const unsigned grid = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((n + cse::kBlockThreads - 1) / cse::kBlockThreads, 8LL * ev->num_cus));
+  hipLaunchKernelGGL(cse::PlusKernel, dim3(grid), dim3(cse::kBlockThreads), 0, ev->stream, d_state,
+                     d_delta, d_state_plus_delta, ev->plus_runs.p, (int)ev->plus_runs_host.size());
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+int cse_plus(cse_evaluator* ev, const double* state, const double* delta,
+             double* state_plus_delta) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (!ev->plus_supported)
+    return Fail(CSE_ERR_UNSUPPORTED, "Plus on device: an active parameter block has a manifold");
+  if (ev->num_parameters == 0) return CSE_OK;
+  if (!state || !delta || !state_plus_delta) return Fail(CSE_ERR_INVALID, "null pointer");
+  CSE_HIP(hipSetDevice(ev->device));
+  int rc;
+  if ((rc = ev->h_state.ensure(ev->num_parameters))) return rc;
+  if ((rc = ev->h_delta.ensure(std::max<int64_t>(1, ev->num_effective)))) return rc;
+  if ((rc = ev->h_plus.ensure(ev->num_parameters))) return rc;
+  CSE_HIP(hipMemcpyAsync(ev->h_state.p, state, ev->num_parameters * sizeof(double),
+                         hipMemcpyHostToDevice, ev->stream));
+  CSE_HIP(hipMemcpyAsync(ev->h_delta.p, delta, ev->num_effective * sizeof(double),
+                         hipMemcpyHostToDevice, ev->stream));
+  double* out = ev->h_plus.p;
+  if ((rc = cse_plus_device(ev, ev->h_state.p, ev->h_delta.p, out))) return rc;
+  CSE_HIP(hipMemcpyAsync(state_plus_delta, out, ev->num_parameters * sizeof(double),
+                         hipMemcpyDeviceToHost, ev->stream));
+  CSE_HIP(hipStreamSynchronize(ev->stream));
+  return CSE_OK;
+}
+
 void cse_destroy(cse_evaluator* ev) {
   if (!ev) return;
   (void)hipSetDevice(ev->device);
@@ -937,6 +1015,9 @@ void cse_destroy(cse_evaluator* ev) {
   ev->jac_offsets.release();
   ev->partials.release();
   ev->partials2.release();
+  ev->plus_runs.release();
+  ev->h_delta.release();
+  ev->h_plus.release();
   ev->status.release();
   ev->h_state.release();
   ev->h_cost.release();

@@ -1502,6 +1502,27 @@ __global__ __launch_bounds__(kWave) void GradientRangeKernel(const GradArgs g) {
   }
 }
 
+// Program::Plus for manifold-free blocks: runs of consecutive state entries
+// whose delta offset is a constant shift away (one run for a BAL problem).
+struct PlusRun {
+  int64_t state_begin;
+  int64_t length;
+  int64_t delta_shift;  // delta index = state index - delta_shift
+};
+
+__global__ __launch_bounds__(kBlockThreads) void PlusKernel(const double* x, const double* delta,
+                                                            double* out, const PlusRun* runs,
+                                                            int num_runs) {
+  for (int r = 0; r < num_runs; ++r) {
+    const PlusRun run = runs[r];
+    for (int64_t t = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x; t < run.length;
+         t += (int64_t)gridDim.x * kBlockThreads) {
+      const int64_t i = run.state_begin + t;
+      out[i] = x[i] + delta[i - run.delta_shift];
+    }
+  }
+}
+
 // First pass of the cost reduction when there are many partials: workgroup
 // b sums partials [b*per, (b+1)*per) in a fixed order.
 __global__ __launch_bounds__(kBlockThreads) void PartialSumKernel(const double* partials,

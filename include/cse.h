@@ -182,6 +182,20 @@ int cse_wait(cse_evaluator* ev);
  * num_plus_jacobian_values doubles. */
 int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians);
 
+/* Replaces Evaluator::Plus -> Program::Plus (internal/ceres/program.cc:121-149,
+ * internal/ceres/parameter_block.h:227-251) for problems whose active
+ * parameter blocks have no manifold: x_plus_delta = x + delta block by block
+ * (state offsets vs delta offsets of the descriptor).  Box constraints are
+ * not part of the descriptor, so none are applied.  Returns
+ * CSE_ERR_UNSUPPORTED when an active block has a manifold (the caller keeps
+ * Ceres' host Plus for those).
+ *   cse_plus_device: device pointers, asynchronous on the evaluator's stream
+ *   cse_plus:        host pointers, synchronous */
+int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_delta,
+                    double* d_state_plus_delta);
+int cse_plus(cse_evaluator* ev, const double* state, const double* delta,
+             double* state_plus_delta);
+
 void cse_destroy(cse_evaluator* ev);
 
 /* Thread-local description of the last error. */

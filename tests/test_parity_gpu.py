@@ -297,3 +297,41 @@ def test_gradient_post_pass_deterministic_and_matches_atomics(gpu):
     assert_parity(a, ref)
     assert np.array_equal(a[3], b[3])
     assert is_approx(atomic[3], a[3], 1e-13)
+
+
+def test_plus_on_device(gpu):
+    # Evaluator::Plus -> Program::Plus (program.cc:121-149): without a
+    # manifold ParameterBlock::Plus is x + delta (parameter_block.h:227-235),
+    # bit for bit.
+    prog = small_bal(C=8, P=300, O_=1200)
+    ev = ca.Evaluator(prog)
+    rng = np.random.default_rng(3)
+    delta = rng.normal(size=prog.num_effective_parameters)
+    out = ev.plus(prog.state, delta)
+    assert np.array_equal(out, prog.state + delta)
+    ev.close()
+
+
+def test_plus_with_ragged_blocks_and_constants(gpu):
+    p = ca.ProblemCUDA()
+    rng = np.random.default_rng(11)
+    cams = [p.add_parameter_block(rng.normal(size=7)) for _ in range(3)]
+    pts = [p.add_parameter_block(rng.normal(size=3)) for _ in range(5)]
+    for i, x in enumerate(pts):
+        p.add_residual_block(ca.SNAVELY_NO_DISTORTION_2_7_3, None, [1.0, 2.0], cams[i % 3], x)
+        p.add_residual_block(ca.POINT_DISPLACEMENT_3_3, None, [0.1, 0.2, 0.3], x)
+    p.set_parameter_block_constant(cams[1])
+    prog = p.program()
+    prog.compile(ca.BLOCK_SPARSE)
+    ev = ca.Evaluator(prog)
+    delta = rng.normal(size=prog.num_effective_parameters)
+    assert np.array_equal(ev.plus(prog.state, delta), prog.state + delta)
+    ev.close()
+
+
+def test_plus_refuses_manifolds(gpu):
+    prog = mini_ba(ca.BLOCK_SPARSE)
+    ev = ca.Evaluator(prog)
+    with pytest.raises(RuntimeError, match="manifold"):
+        ev.plus(prog.state, np.zeros(prog.num_effective_parameters))
+    ev.close()
