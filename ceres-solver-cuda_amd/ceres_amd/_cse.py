@@ -80,7 +80,7 @@ class cse_problem_desc(C.Structure):
 class cse_options(C.Structure):
     _fields_ = [("device", C.c_int32), ("check_finite", C.c_int32),
                 ("apply_loss_function", C.c_int32), ("force_general_layout", C.c_int32),
-                ("profile", C.c_int32), ("reserved", C.c_int32), ("stream", C.c_void_p)]
+                ("profile", C.c_int32), ("use_stream", C.c_int32), ("stream", C.c_void_p)]
 
 
 class cse_info(C.Structure):
@@ -109,6 +109,8 @@ SIGNATURES = {
     "cse_set_plus_jacobians": (C.c_int, [C.c_void_p, P_f64]),
     "cse_plus_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_plus": (C.c_int, [C.c_void_p, P_f64, P_f64, P_f64]),
+    "cse_jacobian_right_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_jacobian_left_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_destroy": (None, [C.c_void_p]),
     "cse_last_error": (C.c_char_p, []),
     "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),

@@ -359,7 +359,10 @@ class Evaluator:
         opts.apply_loss_function = int(apply_loss_function)
         opts.force_general_layout = int(force_general_layout)
         opts.profile = int(profile)
-        opts.stream = stream
+        # stream: a hipStream_t handle (int) to run on -- 0 is the null stream
+        # (torch's default stream); None = an evaluator-owned stream.
+        opts.use_stream = int(stream is not None)
+        opts.stream = stream if stream else None
         h = C.c_void_p()
         _cse.check(L.cse_create(C.byref(self.desc), C.byref(opts), C.byref(h)), "cse_create")
         self.handle = h
@@ -410,6 +413,16 @@ class Evaluator:
         _cse.check(_cse.lib().cse_plus(self.handle, _ptr(state, C.c_double),
                                        _ptr(delta, C.c_double), _ptr(out, C.c_double)), "cse_plus")
         return out
+
+    def right_multiply_device(self, d_jacobian, d_x, d_y):
+        """y += J x on the device (CudaSparseMatrix::RightMultiplyAndAccumulate)."""
+        return _cse.check(_cse.lib().cse_jacobian_right_multiply(self.handle, d_jacobian, d_x, d_y),
+                          "cse_jacobian_right_multiply")
+
+    def left_multiply_device(self, d_jacobian, d_x, d_y):
+        """y += J^T x on the device (CudaSparseMatrix::LeftMultiplyAndAccumulate)."""
+        return _cse.check(_cse.lib().cse_jacobian_left_multiply(self.handle, d_jacobian, d_x, d_y),
+                          "cse_jacobian_left_multiply")
 
     def plus_device(self, d_state, d_delta, d_out):
         """Device-pointer Plus on the evaluator's stream.  Async."""

@@ -713,7 +713,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   if (hipDeviceGetAttribute(&ev->num_cus, hipDeviceAttributeMultiprocessorCount, ev->device) !=
       hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "hipDeviceGetAttribute failed"));
-  if (ev->opts.stream) {
+  if (ev->opts.stream || ev->opts.use_stream) {
     ev->stream = (hipStream_t)ev->opts.stream;
   } else {
     if (hipStreamCreateWithFlags(&ev->stream, hipStreamNonBlocking) != hipSuccess)
@@ -950,6 +950,96 @@ int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians) {
                          hipMemcpyHostToDevice, ev->stream));
   CSE_HIP(hipStreamSynchronize(ev->stream));
   return CSE_OK;
+}
+
+extern "C++" {
+namespace {
+
+template <class K>
+void LaunchMultiply(const cse::GroupArgs& a, bool affine, bool left, const double* x, double* y,
+                    hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + cse::kBlockThreads - 1) / cse::kBlockThreads));
+  if (affine && !left)
+    hipLaunchKernelGGL(cse::RightMultiplyAffineKernel<K>, grid, dim3(cse::kBlockThreads), 0, s, a,
+                       x, y);
+  else if (left)
+    hipLaunchKernelGGL((cse::MultiplyTableKernel<K, true>), grid, dim3(cse::kBlockThreads), 0, s,
+                       a, x, y);
+  else
+    hipLaunchKernelGGL((cse::MultiplyTableKernel<K, false>), grid, dim3(cse::kBlockThreads), 0, s,
+                       a, x, y);
+}
+
+bool DispatchMultiply(int kind, const cse::GroupArgs& a, bool affine, bool left, const double* x,
+                      double* y, hipStream_t s) {
+  switch (kind) {
+    case CSE_FUNCTOR_SNAVELY_2_9_3:
+      return LaunchMultiply<cse::SnavelyKind>(a, affine, left, x, y, s), true;
+    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3:
+      return LaunchMultiply<cse::SnavelyNoDistortionKind>(a, affine, left, x, y, s), true;
+    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3:
+      return LaunchMultiply<cse::SnavelyQuaternionKind>(a, affine, left, x, y, s), true;
+    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3:
+      return LaunchMultiply<cse::PointDisplacementKind>(a, affine, left, x, y, s), true;
+    default:
+      return false;
+  }
+}
+
+int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double* y, bool left) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (!ev->has_layout)
+    return Fail(CSE_ERR_INVALID, "the descriptor had no Jacobian layout");
+  if (!J || !x || !y) return Fail(CSE_ERR_INVALID, "null pointer");
+  CSE_HIP(hipSetDevice(ev->device));
+  for (auto& G : ev->groups) {
+    if (G.n == 0) continue;
+    bool plans = G.affine;
+    for (int j = 0; j < G.shape.nb; ++j) plans = plans && G.grad[j].ready;
+    // MakeArgs wants non-const outputs; the kernels only read a.jacobian.
+    cse::GroupArgs a = MakeArgs(ev, G, nullptr, nullptr, const_cast<double*>(J), nullptr);
+    if (left && plans) {
+      const int sizes[2] = {G.shape.s0, G.shape.s1};
+      for (int j = 0; j < G.shape.nb; ++j) {
+        const Group::GradPlan& P = G.grad[j];
+        cse::GradArgs ga{};
+        ga.jac = J;
+        for (int r = 0; r < G.shape.nr && r < 3; ++r) ga.jrow[r] = G.jac_base[j][r];
+        ga.jstride = G.jac_stride[j];
+        ga.res = x;
+        ga.res_base = G.res_base;
+        ga.perm = P.perm.p;
+        ga.off = P.off.p;
+        ga.count = P.count;
+        ga.lo = P.lo;
+        ga.grad = y;
+        ga.delta_base = G.delta_base[j];
+        if (!LaunchGradPass(G.shape.nr, sizes[j], ga, P, ev->stream))
+          return Fail(CSE_ERR_UNSUPPORTED, "no J^T x pass for this shape");
+      }
+    } else {
+      if (!G.affine && !ev->any_general)
+        return Fail(CSE_ERR_UNSUPPORTED, "table-path tables were not uploaded");
+      if (!DispatchMultiply(G.kind, a, G.affine, left, x, y, ev->stream))
+        return Fail(CSE_ERR_UNSUPPORTED, "no multiply kernel for functor kind " +
+                                             std::to_string(G.kind));
+    }
+    CSE_HIP(hipGetLastError());
+  }
+  return CSE_OK;
+}
+
+}  // namespace
+}  // extern "C++"
+
+int cse_jacobian_right_multiply(cse_evaluator* ev, const double* d_jacobian_values,
+                                const double* d_x, double* d_y) {
+  return JacobianMultiply(ev, d_jacobian_values, d_x, d_y, false);
+}
+
+int cse_jacobian_left_multiply(cse_evaluator* ev, const double* d_jacobian_values,
+                               const double* d_x, double* d_y) {
+  return JacobianMultiply(ev, d_jacobian_values, d_x, d_y, true);
 }
 
 int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_delta,

@@ -1502,6 +1502,84 @@ __global__ __launch_bounds__(kWave) void GradientRangeKernel(const GradArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The Jacobian as a linear operator (cse_jacobian_right/left_multiply):
+// y += J x and y += J^T x on the values this evaluator wrote.  The affine
+// J^T x reuses the gradient post-pass kernels (x in place of r).
+// ---------------------------------------------------------------------------
+template <class K>
+__global__ __launch_bounds__(kBlockThreads) void RightMultiplyAffineKernel(const GroupArgs a,
+                                                                           const double* x,
+                                                                           double* y) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1;
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (i >= a.n) return;
+  const int2 id = LoadIds<K>(a, i);
+  const double* x0 = x + a.delta_base[0] + (int64_t)S0 * id.x;
+  double acc[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const double* row = a.jacobian + a.jac_base[0][k] + a.jac_stride[0] * i;
+    double t = 0.0;
+#pragma unroll
+    for (int c = 0; c < S0; ++c) t += row[c] * x0[c];
+    acc[k] = t;
+  }
+  if constexpr (NB == 2) {
+    const double* x1 = x + a.delta_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double* row = a.jacobian + a.jac_base[1][k] + a.jac_stride[1] * i;
+#pragma unroll
+      for (int c = 0; c < S1; ++c) acc[k] += row[c] * x1[c];
+    }
+  }
+  double* yb = y + a.res_base + (int64_t)NR * i;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) yb[k] += acc[k];
+}
+
+// Table path (any layout, constant blocks, tangent sizes): the reference's
+// WriteJacobians addressing (cuda_evaluator_kernel.h:260-294).
+template <class K, bool kLeft>
+__global__ __launch_bounds__(kBlockThreads) void MultiplyTableKernel(const GroupArgs a,
+                                                                     const double* x, double* y) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1;
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (i >= a.n) return;
+  const int64_t gi = a.gindex ? a.gindex[i] : a.first + i;
+  const int2 ii = LoadIds<K>(a, i);
+  const int32_t ids[2] = {ii.x, ii.y};
+  const int64_t res = a.residual_layout[gi];
+  int64_t q = a.jac_layout[gi];
+  double acc[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) acc[k] = 0.0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const PbDev pb = a.pbs[ids[j]];
+    if (pb.is_constant) continue;
+    const int S = j == 0 ? S0 : S1;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double* row = a.jacobian + a.jac_offsets[q++];
+      for (int c = 0; c < S; ++c) {
+        if (c >= pb.tangent_size) break;
+        if constexpr (kLeft)
+          unsafeAtomicAdd(y + pb.delta_offset + c, row[c] * x[res + k]);
+        else
+          acc[k] += row[c] * x[pb.delta_offset + c];
+      }
+    }
+  }
+  if constexpr (!kLeft) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) y[res + k] += acc[k];
+  }
+}
+
 // Program::Plus for manifold-free blocks: runs of consecutive state entries
 // whose delta offset is a constant shift away (one run for a BAL problem).
 struct PlusRun {

@@ -142,14 +142,15 @@ typedef struct cse_options {
   int32_t apply_loss_function;  /* Evaluator::EvaluateOptions::apply_loss_function */
   int32_t force_general_layout; /* never take the affine fast path (testing) */
   int32_t profile;              /* time every evaluate kernel with HIP events */
-  int32_t reserved;
-  void* stream;                 /* hipStream_t to run on; NULL = evaluator-owned stream */
+  int32_t use_stream;           /* 1: run on `stream` as given, even NULL (the null stream) */
+  void* stream;                 /* hipStream_t to run on; NULL and use_stream 0 =
+                                   an evaluator-owned stream */
 } cse_options;
 
 typedef struct cse_evaluator cse_evaluator;
 
 /* Fills *options with the defaults: device -1, check_finite 1,
- * apply_loss_function 1, everything else 0. */
+ * apply_loss_function 1, everything else 0 (an evaluator-owned stream). */
 void cse_default_options(cse_options* options);
 
 /* Replaces RegisteredCUDAEvaluators::Init + each
@@ -195,6 +196,27 @@ int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_de
                     double* d_state_plus_delta);
 int cse_plus(cse_evaluator* ev, const double* state, const double* delta,
              double* state_plus_delta);
+
+/* The Jacobian as a linear operator on the device (a consumer of
+ * the evaluator's output that keeps it in HBM).  J is d_jacobian_values as
+ * this evaluator writes it (the descriptor's BlockSparse or CompressedRow
+ * layout); x and y are device vectors; asynchronous on the evaluator's
+ * stream.
+ *   cse_jacobian_right_multiply: y += J x  (x: num_effective_parameters,
+ *       y: num_residuals) -- CudaSparseMatrix::RightMultiplyAndAccumulate
+ *       (internal/ceres/cuda_sparse_matrix.h:77), BlockSparseMatrix::
+ *       RightMultiplyAndAccumulate (block_sparse_matrix.h:76)
+ *   cse_jacobian_left_multiply:  y += J^T x (x: num_residuals,
+ *       y: num_effective_parameters) -- LeftMultiplyAndAccumulate
+ *       (cuda_sparse_matrix.h:79, block_sparse_matrix.h:81); deterministic on
+ *       the affine path (per-parameter-block ordered sums), FP64 atomics on
+ *       the table path.
+ * The reference copies the values to the host and back (CopyValuesFromCpu,
+ * cuda_sparse_matrix.h:96); here they never leave HBM. */
+int cse_jacobian_right_multiply(cse_evaluator* ev, const double* d_jacobian_values,
+                                const double* d_x, double* d_y);
+int cse_jacobian_left_multiply(cse_evaluator* ev, const double* d_jacobian_values,
+                               const double* d_x, double* d_y);
 
 void cse_destroy(cse_evaluator* ev);
 

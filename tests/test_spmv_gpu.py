@@ -1,0 +1,141 @@
+"""GPU: the Jacobian as a device linear operator.
+
+cse_jacobian_right_multiply / cse_jacobian_left_multiply act on the values
+the evaluator wrote, in HBM (the reference copies them to the host and back,
+CudaSparseMatrix::CopyValuesFromCpu, cuda_sparse_matrix.h:77-96).  Checked
+against a dense reconstruction of J from the layout tables
+(BlockJacobianWriter / CompressedRowJacobianWriter addressing), on both
+layouts, the affine and the table paths, constant blocks and manifolds; and
+used end to end as the operator of a CGNR solve of the damped normal
+equations (cgnr_solver.cc), compared with a dense solve.
+"""
+import numpy as np
+import pytest
+
+import ceres_amd as ca
+from ceres_amd import bal
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def dense_jacobian(prog, values):
+    """J[residual row, delta column] from the program's layout tables."""
+    J = np.zeros((prog.num_residuals, prog.num_effective_parameters))
+    begin, ids = prog.block_params_csr()
+    nres = prog.residuals_per_block()
+    for b in range(prog.num_residual_blocks):
+        q = int(prog.jacobian_per_residual_layout[b])
+        r0 = int(prog.residual_layout[b])
+        for pid in ids[begin[b]:begin[b + 1]]:
+            if prog.pb_constant[pid]:
+                continue
+            d0, t = int(prog.delta_offset[pid]), int(prog.pb_tangent[pid])
+            for k in range(int(nres[b])):
+                off = int(prog.jacobian_per_residual_offsets[q])
+                q += 1
+                J[r0 + k, d0:d0 + t] = values[off:off + t]
+    return J
+
+
+def device_check(prog, force_general=False, seed=0):
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ev = ca.Evaluator(prog, force_general_layout=force_general, stream=stream)
+    ok, cost, r, g, jvals = ev.evaluate()
+    assert ok
+    J = dense_jacobian(prog, jvals)
+    rng = np.random.default_rng(seed)
+    x = rng.normal(size=prog.num_effective_parameters)
+    y0 = rng.normal(size=prog.num_residuals)
+    f64 = torch.float64
+    dj = torch.from_numpy(jvals).to(dev)
+    dx = torch.from_numpy(x).to(dev)
+    dy = torch.from_numpy(y0.copy()).to(dev)
+    ev.right_multiply_device(dj.data_ptr(), dx.data_ptr(), dy.data_ptr())
+    dz = torch.from_numpy(x.copy()).to(dev)
+    dyl = torch.from_numpy(y0).to(dev)
+    ev.left_multiply_device(dj.data_ptr(), dyl.data_ptr(), dz.data_ptr())
+    torch.cuda.synchronize(dev)
+    y = dy.cpu().numpy()
+    z = dz.cpu().numpy()
+    ev.close()
+    ref_y = y0 + J @ x
+    ref_z = x + J.T @ y0
+    assert np.linalg.norm(y - ref_y) <= 1e-13 * np.linalg.norm(ref_y)
+    assert np.linalg.norm(z - ref_z) <= 1e-13 * np.linalg.norm(ref_z)
+    # J^T r with r the evaluator's residuals is the gradient it returned.
+    return J, r, g, jvals
+
+
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+@pytest.mark.parametrize("general", [False, True])
+def test_jacobian_multiply_matches_dense(gpu, fmt, general):
+    prog = bal.synthetic_program((12, 400, 1600), loss=ca.Loss.huber(1.0), format=fmt, seed=5)
+    J, r, g, _ = device_check(prog, force_general=general)
+    assert np.linalg.norm(J.T @ r - g) <= 1e-13 * np.linalg.norm(g)
+
+
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+def test_jacobian_multiply_mini_ba(gpu, fmt):
+    # Constant blocks and a ProductManifold camera: the table path, local
+    # (tangent-space) Jacobian columns.
+    from test_parity_gpu import mini_ba
+    device_check(mini_ba(fmt))
+
+
+def test_cgnr_on_device_matches_dense_solve(gpu):
+    # One Levenberg-Marquardt step's linear system, (J^T J + lam D) dx = -g
+    # with D = diag(J^T J) (levenberg_marquardt_strategy.cc), solved by
+    # Jacobi-preconditioned conjugate gradients on the normal equations
+    # (cgnr_solver.cc): every J / J^T product through the device operator,
+    # the values never leave HBM.  Compared with a dense solve.
+    prog = bal.synthetic_program((6, 120, 500), loss=ca.Loss.huber(1.0), seed=9)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ev = ca.Evaluator(prog, stream=stream)
+    f64 = torch.float64
+    n, m = prog.num_effective_parameters, prog.num_residuals
+    state = torch.from_numpy(prog.state).to(dev)
+    cost = torch.zeros(1, dtype=f64, device=dev)
+    r = torch.empty(m, dtype=f64, device=dev)
+    jac = torch.empty(prog.num_jacobian_values, dtype=f64, device=dev)
+    g = torch.empty(n, dtype=f64, device=dev)
+    ev.evaluate_device(state.data_ptr(), cost.data_ptr(), r.data_ptr(), g.data_ptr(),
+                       jac.data_ptr())
+    assert ev.wait() == 0
+    J = dense_jacobian(prog, jac.cpu().numpy())
+    lam = 1e-2
+    Dh = np.einsum("ij,ij->j", J, J)
+    D = torch.from_numpy(Dh).to(dev)
+
+    def normal_op(v):
+        Jv = torch.zeros(m, dtype=f64, device=dev)
+        ev.right_multiply_device(jac.data_ptr(), v.data_ptr(), Jv.data_ptr())
+        out = lam * D * v
+        ev.left_multiply_device(jac.data_ptr(), Jv.data_ptr(), out.data_ptr())
+        return out
+
+    b = -g
+    Minv = 1.0 / ((1.0 + lam) * D)
+    x = torch.zeros(n, dtype=f64, device=dev)
+    res = b.clone()
+    z = Minv * res
+    p = z.clone()
+    rz = torch.dot(res, z)
+    for _ in range(1000):
+        Ap = normal_op(p)
+        alpha = rz / torch.dot(p, Ap)
+        x += alpha * p
+        res -= alpha * Ap
+        if res.norm() <= 1e-12 * b.norm():
+            break
+        z = Minv * res
+        rz_new = torch.dot(res, z)
+        p = z + (rz_new / rz) * p
+        rz = rz_new
+    ref = np.linalg.solve(J.T @ J + lam * np.diag(Dh), -(J.T @ r.cpu().numpy()))
+    got = x.cpu().numpy()
+    ev.close()
+    assert np.linalg.norm(got - ref) <= 1e-8 * np.linalg.norm(ref)
