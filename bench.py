@@ -50,11 +50,13 @@ def parse():
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--gradient", action="store_true", help="also produce the gradient J^T r")
-    ap.add_argument("--mode", default="jacobian", choices=["jacobian", "residual", "candidate"],
+    ap.add_argument("--mode", default="jacobian",
+                    choices=["jacobian", "residual", "candidate", "spmv"],
                     help="jacobian: residual+Jacobian evaluation (the headline metric); "
                          "residual: residuals+cost only; candidate: the trust-region candidate "
                          "step, Plus(x, delta) then cost-only evaluation "
-                         "(trust_region_minimizer.cc:770-788)")
+                         "(trust_region_minimizer.cc:770-788); spmv: one CGNR iteration's "
+                         "products J p and J^T (J p) on the evaluated Jacobian (cgnr_solver.cc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-blocks", type=int, default=0,
                     help="0 = the whole workload (about 1 s per eval on 16 cores)")
@@ -162,6 +164,11 @@ def main():
     if args.mode == "candidate":
         delta = torch.full((prog.num_effective_parameters,), 1e-6, dtype=f64, device=dev)
         cand = torch.empty_like(state)
+    if args.mode == "spmv":
+        ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None, jac.data_ptr())
+        pvec = torch.ones(prog.num_effective_parameters, dtype=f64, device=dev)
+        jp = torch.zeros(prog.num_residuals, dtype=f64, device=dev)
+        jtjp = torch.zeros(prog.num_effective_parameters, dtype=f64, device=dev)
 
     def step():
         if args.mode == "jacobian":
@@ -169,9 +176,13 @@ def main():
                                jac.data_ptr())
         elif args.mode == "residual":
             ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None, None)
-        else:
+        elif args.mode == "candidate":
             ev.plus_device(state.data_ptr(), delta.data_ptr(), cand.data_ptr())
             ev.evaluate_device(cand.data_ptr(), cost.data_ptr(), None, None, None)
+        else:
+            ev.right_multiply_device(jac.data_ptr(), pvec.data_ptr(), jp.data_ptr())
+            ev.left_multiply_device(jac.data_ptr(), jp.data_ptr(), jtjp.data_ptr())
+            return
         if world > 1:
             dist.all_reduce(cost)  # RCCL over xGMI: the global cost
 
@@ -194,6 +205,8 @@ def main():
     status = ev.wait()
     last_ms, total_ms, launches = ev.kernel_stats()
     kernel_ms = total_ms / max(launches, 1)
+    if args.mode == "spmv":  # no evaluate launches in the timed loop: the step time
+        kernel_ms = elapsed / args.steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=f64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -248,6 +261,10 @@ def main():
                                                    if args.gradient else 0)
     if args.mode == "residual":
         bytes_per_launch = info.bytes_residual_eval
+    elif args.mode == "spmv":
+        # J read twice, p/J p/J^T J p vectors; kernel_ms (events around the
+        # evaluate launches only) does not apply, the step time does
+        bytes_per_launch = 2 * 8 * prog.num_jacobian_values
     elif args.mode == "candidate":
         # the timed kernel is the cost-only evaluation (no residual stores);
         # Plus is in ms_per_step, not in kernel_ms_avg
@@ -286,7 +303,8 @@ def main():
                 "workload": f"{args.config} SnavelyReprojectionError<2,9,3> "
                             f"{args.loss} {args.format} "
                             + {"jacobian": "residual+Jacobian", "residual": "residual+cost",
-                               "candidate": "Plus + cost-only"}[args.mode]
+                               "candidate": "Plus + cost-only",
+                               "spmv": "J p + J^T (J p)"}[args.mode]
                             + f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
                 "blocks_per_rank": shard_info["blocks"],

@@ -135,6 +135,121 @@ def read(path):
     return cameras, points, cam_idx, pt_idx, obs
 
 
+# --------------------------------------------------------------------------
+# BALProblem::Normalize / Perturb (examples/bal_problem.cc:246-330), angle-axis
+# cameras ([aa 3 | t 3 | f k1 k2]).
+# --------------------------------------------------------------------------
+def angle_axis_rotate(aa, pts):
+    """AngleAxisRotatePoint (rotation.h:830-899), row-wise: Rodrigues, or
+    the first-order form when theta^2 <= DBL_EPSILON."""
+    aa = np.asarray(aa, np.float64)
+    pts = np.asarray(pts, np.float64)
+    th2 = np.einsum("ij,ij->i", aa, aa)
+    big = th2 > np.finfo(np.float64).eps
+    out = pts + np.cross(aa, pts)
+    if big.any():
+        th = np.sqrt(th2[big])
+        w = aa[big] / th[:, None]
+        c, s_ = np.cos(th)[:, None], np.sin(th)[:, None]
+        p = pts[big]
+        wxp = np.cross(w, p)
+        tmp = np.einsum("ij,ij->i", w, p)[:, None] * (1.0 - c)
+        out[big] = p * c + wxp * s_ + w * tmp
+    return out
+
+
+def _median(x):
+    """Median() of bal_problem.cc:64-68: std::nth_element at size/2."""
+    x = np.asarray(x, np.float64)
+    return float(np.partition(x, x.size // 2)[x.size // 2])
+
+
+def camera_to_angle_axis_and_center(cameras):
+    """CameraToAngleAxisAndCenter: c = -R^T t."""
+    aa = cameras[:, 0:3].copy()
+    center = -angle_axis_rotate(-aa, cameras[:, 3:6])
+    return aa, center
+
+
+def angle_axis_and_center_to_camera(aa, center, cameras):
+    """AngleAxisAndCenterToCamera: t = -R c (writes aa and t in place)."""
+    cameras[:, 0:3] = aa
+    cameras[:, 3:6] = -angle_axis_rotate(aa, center)
+
+
+def normalize(cameras, points):
+    """BALProblem::Normalize (bal_problem.cc:246-287): points and camera
+    centers translated by the marginal median and scaled so the median
+    absolute deviation (L1) is 100.  In place; returns (median, scale)."""
+    median = np.array([_median(points[:, i]) for i in range(3)])
+    mad = _median(np.abs(points - median).sum(axis=1))
+    scale = 100.0 / mad
+    points[:] = scale * (points - median)
+    aa, center = camera_to_angle_axis_and_center(cameras)
+    angle_axis_and_center_to_camera(aa, scale * (center - median), cameras)
+    return median, scale
+
+
+class _StdNormal:
+    """libstdc++ std::normal_distribution<double> over std::mt19937
+    (Marsaglia polar method; generate_canonical<double, 53> from two 32-bit
+    draws), so Perturb reproduces the reference's noise bit for bit.  The
+    reference binds a *copy* of its distribution for every PerturbPoint3
+    call (bal_problem.cc:304,321,327), so the saved second value is dropped
+    after each 3-vector: fresh() models that copy."""
+
+    def __init__(self, bitgen):
+        self.bg = bitgen
+
+    def _canonical(self):
+        u1, u2 = (float(v) for v in self.bg.random_raw(2))
+        s = u1
+        s += u2 * 4294967296.0
+        r = s / 18446744073709551616.0
+        return r if r < 1.0 else np.nextafter(1.0, 0.0)
+
+    def draws(self, n, stddev):
+        out, saved = [], None
+        for _ in range(n):
+            if saved is not None:
+                out.append(saved * stddev)
+                saved = None
+                continue
+            while True:
+                x = 2.0 * self._canonical() - 1.0
+                y = 2.0 * self._canonical() - 1.0
+                r2 = x * x + y * y
+                if not (r2 > 1.0 or r2 == 0.0):
+                    break
+            mult = np.sqrt(-2.0 * np.log(r2) / r2)
+            saved = x * mult
+            out.append(y * mult * stddev)
+        return np.array(out)
+
+
+def perturb(cameras, points, rotation_sigma, translation_sigma, point_sigma):
+    """BALProblem::Perturb (bal_problem.cc:289-330), in place, with the
+    reference's own random stream (std::mt19937, default seed 5489).  As in
+    the reference, the rotation noise uses point_sigma as its standard
+    deviation (bal_problem.cc:309-310) and is drawn only when
+    rotation_sigma > 0."""
+    if min(rotation_sigma, translation_sigma, point_sigma) < 0:
+        raise ValueError("sigmas must be non-negative")
+    bg = np.random.MT19937()
+    bg._legacy_seeding(5489)
+    nd = _StdNormal(bg)
+    if point_sigma > 0:
+        for i in range(points.shape[0]):
+            points[i] += nd.draws(3, point_sigma)
+    for i in range(cameras.shape[0]):
+        aa, center = camera_to_angle_axis_and_center(cameras[i:i + 1])
+        if rotation_sigma > 0.0:
+            aa = aa + nd.draws(3, point_sigma)
+        angle_axis_and_center_to_camera(aa, center, cameras[i:i + 1])
+        if translation_sigma > 0.0:
+            cameras[i, 3:6] += nd.draws(3, translation_sigma)
+
+
 def schur_residual_order(pt_idx, num_points):
     """LexicographicallyOrderResidualBlocks (reorder_program.cc:254-336):
     bucket residual blocks by their E block (point), each bucket filled
