@@ -146,10 +146,15 @@ void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 // The shipped affine kernel: one chunk per wave, back-to-back store tail.
-template <class K, int L, bool J, bool Crs, int Co, bool Two = false, int Dbg = 0>
+template <class K, int L, bool J, bool Crs, int Co, bool Two = false, int Dbg = 0,
+          int WPB = cse::kWavesPerBlock>
 void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, Two, Dbg>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
+  if constexpr (WPB != cse::kWavesPerBlock) {
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    num_wg = std::max<int64_t>(1, (chunks + WPB - 1) / WPB);
+  }
+  hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, Two, Dbg, WPB>),
+                     dim3((unsigned)num_wg), dim3(cse::kWave * WPB), 0, s, a);
 }
 
 template <int kStep>
@@ -212,6 +217,8 @@ LaunchFn SnavelyVariant(int v) {
     case 42: return &LaunchChunks<K, L, true, false, 3>;             // register gather
     case 43: return &LaunchChunks<K, L, true, false, 2, true>;       // two-round
     case 44: return &LaunchChunks<K, L, true, false, 2, false, 512>; // plain (not nt) loads
+    case 45: return &LaunchChunks<K, L, true, false, 2, false, 0, 1>;  // one-wave workgroups
+    case 46: return &LaunchChunks<K, L, true, false, 2, false, 0, 2>;  // two-wave workgroups
     default: return nullptr;
   }
 }

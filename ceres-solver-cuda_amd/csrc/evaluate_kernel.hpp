@@ -838,7 +838,7 @@ __device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw)
 // 2 skips every output store (compute floor), 4 skips the LDS transpose
 // (each lane stores its own values at the coalesced positions).
 template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = false,
-          int kDebug = 0>
+          int kDebug = 0, int kWPB = kWavesPerBlock>
 __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
@@ -849,12 +849,12 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
                               : 1;
   constexpr int kCoopLane = kCoop >= 2 ? ((S0 + 1) & ~1) : kCoop == 1 ? S0 : 0;
   constexpr int kStageLane = kCoopLane > kOutLane ? kCoopLane : kOutLane;
-  __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
+  __shared__ double stage[kWPB][kWave * kStageLane];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
-  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
   if (c >= num_chunks) {
     if (lane == 0) a.partials[c] = 0.0;  // the group's partial slots are 4 per workgroup
     return;
@@ -1170,9 +1170,9 @@ __global__ __launch_bounds__(kBlockThreads) void MembenchM1Kernel(const GroupArg
 }
 
 template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = false,
-          int kDebug = 0>
-__global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug>(a);
+          int kDebug = 0, int kWPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWave * kWPB) void EvaluateAffineChunks(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug, kWPB>(a);
 }
 
 // The general (table) path; also runs affine groups when
