@@ -163,6 +163,27 @@ void LaunchM1(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
+// The software-pipelined persistent kernel: one wave per workgroup,
+// $CSE_PIPE_WAVES (default 8) waves per CU, at most one per chunk.
+int64_t PipelinedGrid(int64_t n) {
+  static int per_cu = -1, cus = 256;
+  if (per_cu < 0) {
+    const char* e = getenv("CSE_PIPE_WAVES");
+    per_cu = e && atoi(e) > 0 ? atoi(e) : 8;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const int64_t chunks = (n + cse::kWave - 1) / cse::kWave;
+  return std::max<int64_t>(1, std::min<int64_t>(chunks, (int64_t)cus * per_cu));
+}
+
+template <class K, int L, bool J, bool Crs>
+void LaunchPipelined(const cse::GroupArgs& a, int64_t, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffinePipelined<K, L, J, Crs>),
+                     dim3((unsigned)PipelinedGrid(a.n)), dim3(cse::kWave), 0, s, a);
+}
+
 // Tuning variants of the hot kernel (Snavely, Huber/Trivial, BSM,
 // Jacobian), selected by $CSE_AFFINE_VARIANT: (prefetch, LDS staging,
 // min waves per SIMD).
@@ -219,6 +240,8 @@ LaunchFn SnavelyVariant(int v) {
     case 44: return &LaunchChunks<K, L, true, false, 2, false, 512>; // plain (not nt) loads
     case 45: return &LaunchChunks<K, L, true, false, 2, false, 0, 1>;  // one-wave workgroups
     case 46: return &LaunchChunks<K, L, true, false, 2, false, 0, 2>;  // two-wave workgroups
+    case 47: return &LaunchChunks<K, L, true, false, 2, false, 2048>;  // + per-wave timeline
+    case 48: return &LaunchPipelined<K, L, true, false>;  // software-pipelined persistent
     default: return nullptr;
   }
 }
@@ -321,6 +344,9 @@ struct cse_evaluator {
   std::vector<cse::PlusRun> plus_runs_host;
   DevBuf<cse::PlusRun> plus_runs;
   DevBuf<double> h_delta, h_plus;
+  // Diagnostics: per-wave timestamps of the last evaluation ($CSE_TIMELINE
+  // = output file, written by cse_wait; with CSE_AFFINE_VARIANT=47).
+  DevBuf<uint64_t> timeline;
   DevBuf<int> status;  // [0] running flag, [1] last status
   // Host-path buffers (allocated on first use).
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
@@ -569,6 +595,7 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.gradient = grad;
   a.partials = ev->partials.p + G.partial_offset;
   a.status = ev->status.p;
+  a.timeline = ev->timeline.p;
   a.loss.a = G.loss.a;
   a.loss.scale = G.loss.scale;
   a.loss.scaled = G.loss.scaled;
@@ -885,6 +912,11 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   if (hipMemsetAsync(ev->partials.p, 0, ev->partials.n * sizeof(double), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "hipMemsetAsync failed"));
   if ((rc = ev->partials2.alloc(kPartialBlocks))) return bail(rc);
+  if (getenv("CSE_TIMELINE")) {
+    int64_t waves = 0;
+    for (auto& G : ev->groups) waves = std::max<int64_t>(waves, G.num_wg * cse::kWavesPerBlock);
+    if ((rc = ev->timeline.alloc(std::max<int64_t>(1, waves) * 8))) return bail(rc);
+  }
   if ((rc = ev->status.alloc(2))) return bail(rc);
   if (hipMemsetAsync(ev->status.p, 0, 2 * sizeof(int), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "memset failed"));
@@ -911,6 +943,14 @@ int cse_wait(cse_evaluator* ev) {
   if (ev->opts.profile) {
     int rc = FoldTiming(ev);
     if (rc) return rc;
+  }
+  if (ev->timeline.p) {
+    std::vector<uint64_t> h(ev->timeline.n);
+    CSE_HIP(hipMemcpy(h.data(), ev->timeline.p, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(getenv("CSE_TIMELINE"), "wb")) {
+      fwrite(h.data(), sizeof(uint64_t), h.size(), f);
+      fclose(f);
+    }
   }
   return *ev->status_host ? CSE_EVALUATION_FAILED : CSE_OK;
 }
@@ -1113,6 +1153,7 @@ void cse_destroy(cse_evaluator* ev) {
   ev->partials.release();
   ev->partials2.release();
   ev->plus_runs.release();
+  ev->timeline.release();
   ev->h_delta.release();
   ev->h_plus.release();
   ev->status.release();

@@ -83,6 +83,7 @@ struct GroupArgs {
   double* gradient;
   double* partials;
   int* status;
+  uint64_t* timeline;  // diagnostics only ($CSE_TIMELINE): 8 u64 per wave, or null
   LossParams loss;
   int apply_loss;
   int check_finite;
@@ -777,6 +778,19 @@ __device__ __forceinline__ void SegmentStores(double* seg, int lane, const cse_v
   *keep1 = b1;
 }
 
+// Diagnostics ($CSE_TIMELINE): the shader clock / the 100 MHz real-time
+// clock, read into SGPRs (SMEM, no vector-memory slot).
+__device__ __forceinline__ uint64_t ShaderClock() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+__device__ __forceinline__ uint64_t RealClock() {
+  uint64_t t;
+  asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+
 // A wave-uniform 64-bit value into SGPRs.
 __device__ __forceinline__ uint64_t WaveUniform64(uint64_t x) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
@@ -865,6 +879,12 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int nw = rem < kWave ? (int)rem : kWave;
   const bool active = lane < nw;
   const int64_t i = active ? i0 + lane : a.n - 1;
+  constexpr bool kTime = (kDebug & 2048) != 0;
+  uint64_t tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (kTime) {
+    tl[0] = RealClock();
+    tl[1] = ShaderClock();
+  }
 
   AffineInputs<K> in;
   if constexpr (kCoop == 3) {
@@ -885,6 +905,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     GatherCoop<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
   } else {
     Gather<K>(a, i, LoadIds<K>(a, i), &in);
+  }
+  if constexpr (kTime) {
+    // the gather has landed once its values are used
+    asm volatile("" ::"v"(in.x0[0]), "v"(in.x1[0]), "v"(in.d[0]));
+    tl[2] = ShaderClock();
   }
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok = true;
@@ -916,6 +941,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     AddGradient<K>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0,
                    S1 > 0 ? a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1 : nullptr, S0, S1,
                    r, J0, J1);
+  if constexpr (kTime) {
+    asm volatile("" ::"v"(cost), "v"(r[0]), "v"(J0[0]));
+    tl[3] = ShaderClock();
+  }
   // The wave's cost (fixed xor-butterfly order) and failure flag, before
   // any store is queued.
   double wsum = active ? cost : 0.0;
@@ -1057,6 +1086,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(partial_dst));
   const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, wsum));
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
+  if constexpr (kTime) {
+    KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);  // staging reads landed
+    KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
+    tl[4] = ShaderClock();
+  }
 
   // ---- every store of the wave, back to back ----
   constexpr int kPol = (kDebug >> 4) & 15;  // tuning variants only; 0 = nt sc1
@@ -1073,11 +1107,291 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   // vector store here costs ~10 % of the kernel (tools/membench2.hip, m2).
   ScalarStore64(s_partial, s_wsum);
   if (failed) ScalarStore32(WaveUniform64(reinterpret_cast<uint64_t>(status_dst)), 1u);
+  if constexpr (kTime) {
+    tl[5] = ShaderClock();
+    tl[6] = RealClock();
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    tl[7] = ((uint64_t)xcc << 32) | hw;
+    const uint64_t base = WaveUniform64(reinterpret_cast<uint64_t>(a.timeline + 8 * c));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ScalarStore64(base + 8 * k, tl[k]);
+  }
   asm volatile("s_dcache_wb" ::: "memory");
   KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
   KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
   KeepAlive<kQr>(qr);
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
+}
+
+// ---------------------------------------------------------------------------
+// Software-pipelined persistent variant (Snavely-shaped groups: two slots,
+// the second of size 3, two functor doubles).  Per-wave timelines
+// (tools/timeline.py, CSE_AFFINE_VARIANT=47) of the one-chunk-per-wave
+// kernel show the gather waiting ~10k cycles behind the write stream, half
+// of each wave's life; here every input of chunk c + W (ids, observations,
+// points, cameras) is fetched by LDS-DMA while chunk c computes and stores,
+// and the ids one step earlier still.  All vector-memory traffic of the
+// loop is LDS-DMA or inline-asm stores, so the compiler tracks none of it
+// and the waits are explicit: at the top of an iteration everything but the
+// previous chunk's 13 stores must have landed (s_waitcnt vmcnt(13)).
+// One wave per workgroup (no sibling waves holding a finished wave's slot),
+// persistent over W = gridDim.x waves.
+// ---------------------------------------------------------------------------
+// LDS reads the compiler does not see: its waitcnt pass would otherwise
+// put an s_waitcnt vmcnt(0) (LDS-DMA -> ds_read) at the top of the pipelined
+// loop and drain the previous chunk's stores.  The caller waits lgkmcnt(0)
+// itself (PipeLdsFence) before using the values.
+__device__ __forceinline__ uint32_t LdsAddr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <int kOff>
+__device__ __forceinline__ cse_v4i LdsRead128(uint32_t addr) {
+  cse_v4i v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(kOff));
+  return v;
+}
+template <int kOff>
+__device__ __forceinline__ double LdsRead64(uint32_t addr) {
+  double v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(kOff));
+  return v;
+}
+template <int kOff>
+__device__ __forceinline__ int LdsRead32(uint32_t addr) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(kOff));
+  return v;
+}
+__device__ __forceinline__ void V4iToDoubles(cse_v4i v, double* d) { __builtin_memcpy(d, &v, 16); }
+
+// LDS-DMA issue helpers of EvaluateAffinePipelined.  gfx950's
+// global_load_lds moves 1, 2, 4, 12 or 16 bytes per lane and writes lane l's
+// bytes at lds + size * l: the ids go as two dword streams, the 24-byte
+// points as 128 cooperative 12-byte halves (point t at lds + 24 t), the
+// cameras as 16-byte pieces (GatherCoopDma).  (Plain functions: clang drops a
+// kernel whose lambdas capture __shared__ arrays by reference.)
+__device__ __forceinline__ int64_t PipeBlock(const GroupArgs& a, int64_t cc, int lane) {
+  const int64_t i = cc * kWave + lane;
+  return i < a.n ? i : a.n - 1;
+}
+__device__ __forceinline__ void PipeIssueIds(const GroupArgs& a, int64_t cc, int lane, int32_t* ids) {
+  const int32_t* src = a.ids + 2 * PipeBlock(a, cc, lane);
+  __builtin_amdgcn_global_load_lds(src, ids, 4, 0, 2);
+  __builtin_amdgcn_global_load_lds(src + 1, ids + kWave, 4, 0, 2);
+}
+template <int S0p>
+__device__ __forceinline__ void PipeIssueGather(const GroupArgs& a, int64_t cc, int lane, int2 id,
+                                                double* cam, double* obs, double* pt) {
+  constexpr int kPieces = S0p / 2;
+  const int cid_own = id.x - a.packed0_lo;
+#pragma unroll
+  for (int k = 0; k < kPieces; ++k) {
+    const int p = k * kWave + lane;
+    const int t = p / kPieces, q = p - t * kPieces;
+    const int cid = __shfl(cid_own, t, kWave);
+    __builtin_amdgcn_global_load_lds(a.packed0 + (int64_t)S0p * cid + 2 * q, cam + 2 * kWave * k, 16,
+                                     0, 0);
+  }
+  __builtin_amdgcn_global_load_lds(a.data + 2 * PipeBlock(a, cc, lane), obs, 16, 0, 2);
+  const double* base = a.state + a.state_base[1];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = k * kWave + lane;
+    const int pid = __shfl(id.y, p >> 1, kWave);
+    const char* src = reinterpret_cast<const char*>(base + 3 * (int64_t)pid) + 12 * (p & 1);
+    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<char*>(pt) + 12 * kWave * k, 12, 0, 2);
+  }
+}
+
+template <class K, int kLoss, bool kJac, bool kCrs>
+__global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs a) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
+  static_assert(Tr::NB == 2 && S1 == 3 && Tr::D == 2 && NR == 2, "Snavely-shaped groups only");
+  constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kOutLane = kJac ? (kCrs ? NR * N : NR * (S0 + S1)) : 1;
+  constexpr int kQ0 = kJac ? (kCrs ? NR * N / 2 : NR * S0 / 2) : 0;
+  constexpr int kQ1 = (kJac && !kCrs) ? NR * S1 / 2 : 0;
+  __shared__ double in_cam[kWave * S0p];
+  __shared__ double in_obs[kWave * 2];
+  __shared__ double in_pt[3 * kWave];
+  __shared__ int32_t in_ids[2 * kWave];  // id0 of the 64 blocks, then id1
+  __shared__ double stage[kWave * kOutLane];
+
+  const int lane = threadIdx.x;
+  const int64_t nchunks = (a.n + kWave - 1) / kWave;
+  const int64_t W = gridDim.x;
+  int64_t c = blockIdx.x;
+  if (c >= nchunks) return;
+  // Prologue: ids(c), then gather(c) and ids(c + W).
+  PipeIssueIds(a, c, lane, in_ids);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  int2 idc = make_int2(in_ids[lane], in_ids[kWave + lane]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  PipeIssueGather<S0p>(a, c, lane, idc, in_cam, in_obs, in_pt);
+  PipeIssueIds(a, c + W < nchunks ? c + W : nchunks - 1, lane, in_ids);
+  bool first = true;
+  bool prev_fast = true;  // the previous chunk issued exactly kStores stores
+  bool failed_any = false;
+  constexpr int kStores = kQ0 + kQ1 + 1;  // vector stores per full chunk
+  static_assert(kStores <= 63, "vmcnt field");
+  const bool exact = a.residuals != nullptr && (!kJac || a.jacobian != nullptr);
+
+  for (; c < nchunks; c += W) {
+    // Everything issued before the previous chunk's kStores stores has
+    // landed (vmcnt counts in issue order).  Without both outputs the store
+    // count differs: wait for everything (correct, not pipelined).
+    if (first || !exact || !prev_fast)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kStores) : "memory");
+    first = false;
+    __builtin_amdgcn_wave_barrier();
+    AffineInputs<K> in;
+    in.id0 = idc.x;
+    in.id1 = idc.y;
+    int2 idn;
+    {
+      static_assert(S0p == 10, "camera read below assumes 5 pieces");
+      const uint32_t acam = LdsAddr(in_cam) + 8 * S0p * lane;
+      const uint32_t aobs = LdsAddr(in_obs) + 16 * lane;
+      const uint32_t apt = LdsAddr(in_pt) + 24 * lane;
+      const uint32_t aid = LdsAddr(in_ids) + 4 * lane;
+      cse_v4i c0 = LdsRead128<0>(acam), c1 = LdsRead128<16>(acam), c2 = LdsRead128<32>(acam);
+      cse_v4i c3 = LdsRead128<48>(acam), c4 = LdsRead128<64>(acam);
+      cse_v4i ob = LdsRead128<0>(aobs);
+      double p0 = LdsRead64<0>(apt), p1 = LdsRead64<8>(apt), p2 = LdsRead64<16>(apt);
+      int i0 = LdsRead32<0>(aid), i1 = LdsRead32<4 * kWave>(aid);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4)
+                   : : "memory");
+      asm volatile("" : "+v"(ob), "+v"(p0), "+v"(p1), "+v"(p2), "+v"(i0), "+v"(i1));
+      double cam[10];
+      V4iToDoubles(c0, cam);
+      V4iToDoubles(c1, cam + 2);
+      V4iToDoubles(c2, cam + 4);
+      V4iToDoubles(c3, cam + 6);
+      V4iToDoubles(c4, cam + 8);
+#pragma unroll
+      for (int k = 0; k < S0; ++k) in.x0[k] = cam[k];
+      V4iToDoubles(ob, in.d);
+      in.x1[0] = p0;
+      in.x1[1] = p1;
+      in.x1[2] = p2;
+      idn = make_int2(i0, i1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // Next chunk's inputs (clamped past the end: harmless re-reads).
+    const int64_t cn = c + W < nchunks ? c + W : nchunks - 1;
+    const int64_t cnn = c + 2 * W < nchunks ? c + 2 * W : nchunks - 1;
+    PipeIssueGather<S0p>(a, cn, lane, idn, in_cam, in_obs, in_pt);
+    PipeIssueIds(a, cnn, lane, in_ids);
+
+    const int64_t i0 = c * kWave;
+    const int64_t rem = a.n - i0;
+    const int nw = rem < kWave ? (int)rem : kWave;
+    const bool active = lane < nw;
+    double r[NR], J0[NR * S0], J1[NR * S1p];
+    bool ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
+    if (ok && a.check_finite) {
+      bool bad = AnyNonFinite<NR>(r);
+      if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
+      ok = !bad;
+    }
+    const double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+    double wsum = active ? cost : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
+    failed_any = failed_any || (__ballot(active && !ok) != 0);
+    const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(a.partials + c));
+    const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, wsum));
+
+    if (!FastTail<K, kJac, kCrs>(a, i0, nw)) {
+      // Only the group's last, partial chunk: the generic staged stores
+      // (compiler-visible; nothing is waited on after them).
+      StageAndStore<K, kJac, kCrs, true, true>(a, stage, lane, active, i0, nw, r, J0, J1);
+      ScalarStore64(s_partial, s_wsum);
+      idc = idn;
+      prev_fast = false;
+      continue;
+    }
+    const bool jac = kJac && a.jacobian != nullptr;
+    cse_v4i q0[kQ0 > 0 ? kQ0 : 1], q1[kQ1 > 0 ? kQ1 : 1];
+    double* seg0 = nullptr;
+    double* seg1 = nullptr;
+    if constexpr (kJac) {
+      if (jac) {
+        if constexpr (kCrs) {
+          const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0]
+                                                                   : a.jac_base[1][0];
+#pragma unroll
+          for (int k = 0; k < NR; ++k) {
+            const int c0 = (int)(a.jac_base[0][k] - row0);
+            const int c1 = (int)(a.jac_base[1][k] - row0);
+#pragma unroll
+            for (int cc = 0; cc < S0; ++cc) stage[lane * NR * N + c0 + cc] = J0[k * S0 + cc];
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) stage[lane * NR * N + c1 + cc] = J1[k * S1p + cc];
+          }
+          seg0 = a.jacobian + row0 + (int64_t)NR * N * i0;
+        } else {
+          double* st1 = stage + kWave * NR * S0;
+#pragma unroll
+          for (int p = 0; p < NR * S0; ++p) stage[lane * NR * S0 + p] = J0[p];
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) st1[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+          seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+          seg1 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < kQ0; ++j) {
+          const double2 v = reinterpret_cast<const double2*>(stage)[j * kWave + lane];
+          q0[j] = AsV4i(v.x, v.y);
+        }
+        if constexpr (kQ1 > 0) {
+          const double* st1 = stage + kWave * NR * S0;
+#pragma unroll
+          for (int j = 0; j < kQ1; ++j) {
+            const double2 v = reinterpret_cast<const double2*>(st1)[j * kWave + lane];
+            q1[j] = AsV4i(v.x, v.y);
+          }
+        }
+      }
+    }
+    const cse_v4i qr = AsV4i(r[0], r[1]);
+    double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;
+    double *f0 = nullptr, *f1 = nullptr, *e0 = nullptr, *e1 = nullptr;
+    if (jac) {
+      f0 = seg0 + 2 * lane + 512;
+      f1 = seg0 + 2 * lane + 1536;
+      if constexpr (kQ1 > 0) {
+        e0 = seg1 + 2 * lane + 512;
+        e1 = seg1 + 2 * lane + 1536;
+      }
+    }
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
+    // Exactly 13 vector stores per full chunk for the wait at the top (the
+    // Jacobian-less and residual-less forms are not pipelined: host check).
+    if (jac) {
+      SegmentStoresFrom<0, kQ0>(f0, f1, q0);
+      if constexpr (kQ1 > 0) SegmentStoresFrom<0, kQ1>(e0, e1, q1);
+    }
+    if (a.residuals) StoreNt16<0>(rdst, qr);
+    ScalarStore64(s_partial, s_wsum);
+    KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
+    KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(qr));
+    idc = idn;
+  }
+  if (failed_any) ScalarStore32(WaveUniform64(reinterpret_cast<uint64_t>(a.status)), 1u);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave ends
+  asm volatile("s_dcache_wb" ::: "memory");
 }
 
 // Diagnostic only: tools/membench2.hip's m1 memory path (camera gather
