@@ -242,6 +242,13 @@ LaunchFn SnavelyVariant(int v) {
     case 46: return &LaunchChunks<K, L, true, false, 2, false, 0, 2>;  // two-wave workgroups
     case 47: return &LaunchChunks<K, L, true, false, 2, false, 2048>;  // + per-wave timeline
     case 48: return &LaunchPipelined<K, L, true, false>;  // software-pipelined persistent
+    // How the per-wave cost partial is stored (default: lane 0, default
+    // policy, after the output segments).
+    case 49: return &LaunchChunks<K, L, true, false, 2, false, 4096>;   // partial nt sc1
+    case 50: return &LaunchChunks<K, L, true, false, 2, false, 8192>;   // partial sc1
+    case 51: return &LaunchChunks<K, L, true, false, 2, false, 16384>;  // partial first
+    case 52: return &LaunchChunks<K, L, true, false, 2, false, 65536>;  // XCD-grouped slots
+    case 53: return &LaunchChunks<K, L, true, false, 2, false, 32768>;  // no partial (diag.)
     default: return nullptr;
   }
 }
@@ -861,8 +868,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
     }
     // Every kernel writes one cost partial per wave.
+    // Slots are reserved for a multiple of 8 workgroups (the XCD-grouped
+    // slot order, cse::PartialSlot); unused slots stay zero.
     G.partial_offset = ev->total_wg;
-    ev->total_wg += G.num_wg * cse::kWavesPerBlock;
+    ev->total_wg += (G.num_wg + 7) / 8 * 8 * cse::kWavesPerBlock;
     // The LDS-DMA gather reads slot 0 from a repacked copy refreshed every
     // evaluation; worth it while the slot-0 id range is small (BAL: the
     // cameras), otherwise gather 8-byte pieces from the state directly.

@@ -791,20 +791,33 @@ __device__ __forceinline__ uint64_t RealClock() {
   return t;
 }
 
-// A wave-uniform 64-bit value into SGPRs.
-__device__ __forceinline__ uint64_t WaveUniform64(uint64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
-  return ((uint64_t)hi << 32) | lo;
+// Vector stores of one wave-uniform value, issued by the calling lanes
+// (the caller masks to lane 0).  Both operands are VGPRs computed before
+// the store tail, so nothing after the tail writes a VGPR a queued store
+// still has to read.  kPol: 0 = default policy (the partial's line is
+// shared by 16 waves and merges in L2), 1 = nt sc1 (as the output
+// segments), 2 = sc1.
+template <int kPol = 0>
+__device__ __forceinline__ void StoreB64(double* addr, double value) {
+  if constexpr (kPol == 1)
+    asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(addr), "v"(value) : "memory");
+  else if constexpr (kPol == 2)
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(addr), "v"(value) : "memory");
+  else
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(addr), "v"(value) : "memory");
+}
+__device__ __forceinline__ void StoreB32(int* addr, int value) {
+  asm volatile("global_store_dword %0, %1, off" ::"v"(addr), "v"(value) : "memory");
 }
 
-// Scalar (SMEM) stores of wave-uniform values; the caller issues
-// s_dcache_wb before the wave ends.
-__device__ __forceinline__ void ScalarStore64(uint64_t addr, uint64_t value) {
-  asm volatile("s_store_dwordx2 %0, %1, 0x0 glc" ::"s"(value), "s"(addr) : "memory");
-}
-__device__ __forceinline__ void ScalarStore32(uint64_t addr, uint32_t value) {
-  asm volatile("s_store_dword %0, %1, 0x0 glc" ::"s"(value), "s"(addr) : "memory");
+// XCD-grouped cost-partial slots: workgroups are dealt round-robin over
+// the 8 XCDs, so workgroups b, b + 8, b + 16, b + 24 (one XCD, running at
+// about the same time) get one 128-byte line of partials together instead
+// of sharing it with three other XCDs.  The slot space is a multiple of 8
+// workgroups (the host reserves it; unused slots stay zero).
+__device__ __forceinline__ int64_t PartialSlot(int64_t b, int64_t num_wg, int wave, int wpb) {
+  const int64_t per_xcd = (num_wg + 7) / 8;
+  return ((b & 7) * per_xcd + (b >> 3)) * wpb + wave;
 }
 
 template <int kCount>
@@ -869,8 +882,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int wave = threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
   const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
+  double* partial_dst =
+      a.partials + ((kDebug & 65536) ? PartialSlot(blockIdx.x, gridDim.x, wave, kWPB) : c);
   if (c >= num_chunks) {
-    if (lane == 0) a.partials[c] = 0.0;  // the group's partial slots are 4 per workgroup
+    if (lane == 0) *partial_dst = 0.0;  // the group's partial slots are 4 per workgroup
     return;
   }
   double* st = stage[wave];
@@ -951,7 +966,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
   const bool failed = __ballot(active && !ok) != 0;
-  double* partial_dst = a.partials + c;
   int* status_dst = a.status;
 
   if constexpr ((kDebug & 2) != 0) {
@@ -1083,9 +1097,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       e1 = seg1 + 2 * lane + 1536;
     }
   }
-  const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(partial_dst));
-  const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, wsum));
-  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
+  // The partial's address and value in VGPRs now, not after the tail.
+  double* v_partial = partial_dst;
+  double v_wsum = wsum;
+  asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
+  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
   if constexpr (kTime) {
     KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);  // staging reads landed
     KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
@@ -1094,6 +1110,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 
   // ---- every store of the wave, back to back ----
   constexpr int kPol = (kDebug >> 4) & 15;  // tuning variants only; 0 = nt sc1
+  constexpr int kPartPol = (kDebug >> 12) & 3;       // tuning variants only
+  constexpr bool kPartFirst = (kDebug & 16384) != 0;  // tuning variant: partial first
+  if (kPartFirst && lane == 0) StoreB64<kPartPol>(v_partial, v_wsum);
   if (jac) {
     SegmentStoresFrom<0, kQ0, kPol>(f0, f1, q0);
     if constexpr (kQ1 > 0) SegmentStoresFrom<0, kQ1, kPol>(e0, e1, q1);
@@ -1103,10 +1122,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kQr >= 2) StoreNt16<16, kPol>(rdst, qr[1]);
     if constexpr (kQr >= 3) StoreNt16<32, kPol>(rdst, qr[2]);
   }
-  // The cost partial (and the failure flag) by scalar stores: a one-lane
-  // vector store here costs ~10 % of the kernel (tools/membench2.hip, m2).
-  ScalarStore64(s_partial, s_wsum);
-  if (failed) ScalarStore32(WaveUniform64(reinterpret_cast<uint64_t>(status_dst)), 1u);
+  // The cost partial (one per wave, lane 0) and the failure flag, last.
+  if (lane == 0) {
+    if (!kPartFirst && (kDebug & 32768) == 0) StoreB64<kPartPol>(v_partial, v_wsum);
+    if (failed) StoreB32(status_dst, 1);
+  }
   if constexpr (kTime) {
     tl[5] = ShaderClock();
     tl[6] = RealClock();
@@ -1114,15 +1134,15 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     tl[7] = ((uint64_t)xcc << 32) | hw;
-    const uint64_t base = WaveUniform64(reinterpret_cast<uint64_t>(a.timeline + 8 * c));
+    uint64_t mine = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ScalarStore64(base + 8 * k, tl[k]);
+    for (int k = 0; k < 8; ++k) mine = lane == k ? tl[k] : mine;
+    if (lane < 8) a.timeline[8 * c + lane] = mine;
   }
-  asm volatile("s_dcache_wb" ::: "memory");
   KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
   KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
   KeepAlive<kQr>(qr);
-  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
+  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(v_partial), "v"(v_wsum));
 }
 
 // ---------------------------------------------------------------------------
@@ -1237,7 +1257,7 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
   bool first = true;
   bool prev_fast = true;  // the previous chunk issued exactly kStores stores
   bool failed_any = false;
-  constexpr int kStores = kQ0 + kQ1 + 1;  // vector stores per full chunk
+  constexpr int kStores = kQ0 + kQ1 + 2;  // vector stores per full chunk (+ the partial)
   static_assert(kStores <= 63, "vmcnt field");
   const bool exact = a.residuals != nullptr && (!kJac || a.jacobian != nullptr);
 
@@ -1306,14 +1326,15 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
     failed_any = failed_any || (__ballot(active && !ok) != 0);
-    const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(a.partials + c));
-    const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, wsum));
+    double* v_partial = a.partials + c;
+    double v_wsum = wsum;
+    asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
 
     if (!FastTail<K, kJac, kCrs>(a, i0, nw)) {
       // Only the group's last, partial chunk: the generic staged stores
       // (compiler-visible; nothing is waited on after them).
       StageAndStore<K, kJac, kCrs, true, true>(a, stage, lane, active, i0, nw, r, J0, J1);
-      ScalarStore64(s_partial, s_wsum);
+      if (lane == 0) StoreB64(v_partial, v_wsum);
       idc = idn;
       prev_fast = false;
       continue;
@@ -1375,23 +1396,24 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
         e1 = seg1 + 2 * lane + 1536;
       }
     }
-    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
-    // Exactly 13 vector stores per full chunk for the wait at the top (the
-    // Jacobian-less and residual-less forms are not pipelined: host check).
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
+    // Exactly kStores vector stores per full chunk for the wait at the top
+    // (the Jacobian-less and residual-less forms are not pipelined: host
+    // check).
     if (jac) {
       SegmentStoresFrom<0, kQ0>(f0, f1, q0);
       if constexpr (kQ1 > 0) SegmentStoresFrom<0, kQ1>(e0, e1, q1);
     }
     if (a.residuals) StoreNt16<0>(rdst, qr);
-    ScalarStore64(s_partial, s_wsum);
+    if (lane == 0) StoreB64(v_partial, v_wsum);
     KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
     KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
-    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(qr));
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(qr), "v"(v_partial),
+                 "v"(v_wsum));
     idc = idn;
   }
-  if (failed_any) ScalarStore32(WaveUniform64(reinterpret_cast<uint64_t>(a.status)), 1u);
+  if (failed_any && lane == 0) StoreB32(a.status, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave ends
-  asm volatile("s_dcache_wb" ::: "memory");
 }
 
 // Diagnostic only: tools/membench2.hip's m1 memory path (camera gather
@@ -1399,7 +1421,7 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
 // evaluator's real buffers (BSM, Snavely shapes).  Wrong results by design.
 // kStep walks it towards EvaluateAffineChunks one change at a time:
 //   0 m1 as in membench (register gather, compiler stores, lane-0 partial)
-//   1 + the shipped tail (asm stores at SegmentStoresFrom bases, scalar partial)
+//   1 + the shipped tail (asm stores at SegmentStoresFrom bases, lane-0 partial last)
 //   2 + LDS-DMA camera gather (GatherCoopDma)
 //   3 + distinct data per store (q[j] = v * j)
 template <int kStep>
@@ -1469,17 +1491,18 @@ __global__ __launch_bounds__(kBlockThreads) void MembenchM1Kernel(const GroupArg
     double* f1 = seg0 + 2 * lane + 1536;
     double* e0 = seg1 + 2 * lane + 512;
     double* e1 = seg1 + 2 * lane + 1536;
-    const uint64_t s_partial = WaveUniform64(reinterpret_cast<uint64_t>(a.partials + c));
-    const uint64_t s_wsum = WaveUniform64(__builtin_bit_cast(uint64_t, v));
-    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "s"(s_partial), "s"(s_wsum));
+    double* v_partial = a.partials + c;
+    double v_zero = 0.0;
+    asm volatile("" : "+v"(v_partial), "+v"(v_zero));
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
     SegmentStoresFrom<0, 9>(f0, f1, q0);
     SegmentStoresFrom<0, 3>(e0, e1, q1);
     StoreNt16<0>(rdst, qr);
-    ScalarStore64(s_partial, 0);
-    asm volatile("s_dcache_wb" ::: "memory");
+    if (lane == 0) StoreB64(v_partial, v_zero);
     KeepAlive<9>(q0);
     KeepAlive<3>(q1);
-    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(qr));
+    asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(qr), "v"(v_partial),
+                 "v"(v_zero));
   }
 }
 

@@ -283,7 +283,7 @@ def test_problem_13682_full_size(gpu):
     assert_parity(got, ref, "problem-13682")
 
 
-def test_gradient_post_pass_deterministic_and_matches_atomics(gpu):
+def test_gradient_post_pass_deterministic_and_agrees_with_atomics(gpu):
     # Affine groups sum J^T r per parameter block in a fixed order (no
     # atomics): bit-identical run to run, and equal (to the tolerance) to the
     # in-kernel atomic path that serves gradient-without-Jacobian requests.

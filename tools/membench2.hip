@@ -641,12 +641,8 @@ __global__ __launch_bounds__(256) void m2(const int2* ids, const double2* obs, c
   }
   if constexpr (kP == 3) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(pw), "v"(v) : "memory");
   if constexpr (kP == 4) {
-    // scalar store of the wave's value (SMEM path, no vector-memory slot)
-    const long pa = (long)(unsigned)__builtin_amdgcn_readfirstlane((int)((uintptr_t)pp)) |
-                    ((long)__builtin_amdgcn_readfirstlane((int)((uintptr_t)pp >> 32)) << 32);
-    const long vb = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)vb), hi = __builtin_amdgcn_readfirstlane((int)(vb >> 32));
-    asm volatile("s_store_dwordx2 %1, %0, 0x0 glc\n s_dcache_wb" ::"s"(pa), "s"(((long)hi << 32) | (unsigned)lo) : "memory");
+    // lane-0 partial with the output segments' streaming policy
+    if (lane == 0) asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(pp), "v"(v) : "memory");
   }
   asm volatile("" ::"v"(pr), "v"(pe), "v"(pf), "v"(d), "v"(v));
 #pragma unroll
@@ -777,7 +773,7 @@ int main(int argc, char** argv) {
 #define M1(V, label) run(label, rbytes + wbytes, [&] { hipLaunchKernelGGL(m1<V>, dim3(g), dim3(256), 0, 0, ids, obs, pts, cam80, res, E, F_, sink, chunks, (long)kO); });
 #define M2(V, label) run(label, rbytes + wbytes, [&] { hipLaunchKernelGGL(m2<V>, dim3(g), dim3(256), 0, 0, ids, obs, pts, cam80, res, E, F_, sink, chunks, (long)kO); });
   M2(0, "m2 no partial") M2(1, "m2 lane0 partial after") M2(2, "m2 lane0 partial before")
-  M2(3, "m2 wave-wide 8B store after") M2(4, "m2 scalar store after") M2(5, "m2 positive offsets") M2(0, "m2 no partial")
+  M2(3, "m2 wave-wide 8B store after") M2(4, "m2 lane-0 nt sc1 store after") M2(5, "m2 positive offsets") M2(0, "m2 no partial")
   M2(6, "m2 12 quads same data") M2(7, "m2 12 quads random data") M2(8, "m2 12 quads lane-uniform")
   M2(6, "m2 12 quads same data")
   M1(0, "m1 same-value")
