@@ -184,6 +184,33 @@ void LaunchPipelined(const cse::GroupArgs& a, int64_t, hipStream_t s) {
                      dim3((unsigned)PipelinedGrid(a.n)), dim3(cse::kWave), 0, s, a);
 }
 
+// The persistent stream kernel: one wave per workgroup, $CSE_STREAM_WAVES
+// (default 4: one per SIMD) waves per CU, at most one per chunk.
+int64_t StreamGrid(int64_t n) {
+  static int per_cu = -1, cus = 256;
+  if (per_cu < 0) {
+    const char* e = getenv("CSE_STREAM_WAVES");
+    per_cu = e && atoi(e) > 0 ? atoi(e) : 4;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const int64_t chunks = (n + cse::kWave - 1) / cse::kWave;
+  return std::max<int64_t>(1, std::min<int64_t>(chunks, (int64_t)cus * per_cu));
+}
+
+template <class K, int L, int kSets>
+void LaunchStream(const cse::GroupArgs& a, int64_t, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineStream<K, L, kSets>), dim3((unsigned)StreamGrid(a.n)),
+                     dim3(cse::kWave), 0, s, a);
+}
+
+template <class K, int L, int kSets>
+void LaunchStream2(const cse::GroupArgs& a, int64_t, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineStream2<K, L, kSets>), dim3((unsigned)StreamGrid(a.n)),
+                     dim3(cse::kWave), 0, s, a);
+}
+
 // Tuning variants of the hot kernel (Snavely, Huber/Trivial, BSM,
 // Jacobian), selected by $CSE_AFFINE_VARIANT: (prefetch, LDS staging,
 // min waves per SIMD).
@@ -249,6 +276,11 @@ LaunchFn SnavelyVariant(int v) {
     case 51: return &LaunchChunks<K, L, true, false, 2, false, 16384>;  // partial first
     case 52: return &LaunchChunks<K, L, true, false, 2, false, 65536>;  // XCD-grouped slots
     case 53: return &LaunchChunks<K, L, true, false, 2, false, 32768>;  // no partial (diag.)
+    case 54: return &LaunchStream<K, L, 4>;  // persistent stream, 4 store register sets
+    case 55: return &LaunchStream<K, L, 2>;  // 2 sets
+    case 56: return &LaunchStream<K, L, 1>;  // 1 set (the register hazard kept: A/B)
+    case 57: return &LaunchStream2<K, L, 2>;  // 2 waves per SIMD, 2 sets, two-round staging
+    case 58: return &LaunchStream2<K, L, 1>;  // 2 waves per SIMD, 1 set
     default: return nullptr;
   }
 }

@@ -1188,10 +1188,12 @@ __device__ __forceinline__ void V4iToDoubles(cse_v4i v, double* d) { __builtin_m
 
 // LDS-DMA issue helpers of EvaluateAffinePipelined.  gfx950's
 // global_load_lds moves 1, 2, 4, 12 or 16 bytes per lane and writes lane l's
-// bytes at lds + size * l: the ids go as two dword streams, the 24-byte
-// points as 128 cooperative 12-byte halves (point t at lds + 24 t), the
-// cameras as 16-byte pieces (GatherCoopDma).  (Plain functions: clang drops a
-// kernel whose lambdas capture __shared__ arrays by reference.)
+// bytes at lds + size * l -- except the 12-byte form, which writes at
+// lds + 16 * l (measured, tools/ldsdma_probe.hip: a 4-byte hole after each
+// lane's 12 bytes).  The ids go as two dword streams, the 24-byte points as
+// 128 cooperative 12-byte halves (half h of point t at lds + 32 t + 16 h),
+// the cameras as 16-byte pieces (GatherCoopDma).  (Plain functions: clang
+// drops a kernel whose lambdas capture __shared__ arrays by reference.)
 __device__ __forceinline__ int64_t PipeBlock(const GroupArgs& a, int64_t cc, int lane) {
   const int64_t i = cc * kWave + lane;
   return i < a.n ? i : a.n - 1;
@@ -1221,7 +1223,7 @@ __device__ __forceinline__ void PipeIssueGather(const GroupArgs& a, int64_t cc, 
     const int p = k * kWave + lane;
     const int pid = __shfl(id.y, p >> 1, kWave);
     const char* src = reinterpret_cast<const char*>(base + 3 * (int64_t)pid) + 12 * (p & 1);
-    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<char*>(pt) + 12 * kWave * k, 12, 0, 2);
+    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<char*>(pt) + 16 * kWave * k, 12, 0, 2);
   }
 }
 
@@ -1236,7 +1238,7 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
   constexpr int kQ1 = (kJac && !kCrs) ? NR * S1 / 2 : 0;
   __shared__ double in_cam[kWave * S0p];
   __shared__ double in_obs[kWave * 2];
-  __shared__ double in_pt[3 * kWave];
+  __shared__ double in_pt[4 * kWave];  // point t: halves at 32 t and 32 t + 16 bytes
   __shared__ int32_t in_ids[2 * kWave];  // id0 of the 64 blocks, then id1
   __shared__ double stage[kWave * kOutLane];
 
@@ -1279,16 +1281,22 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
       static_assert(S0p == 10, "camera read below assumes 5 pieces");
       const uint32_t acam = LdsAddr(in_cam) + 8 * S0p * lane;
       const uint32_t aobs = LdsAddr(in_obs) + 16 * lane;
-      const uint32_t apt = LdsAddr(in_pt) + 24 * lane;
+      const uint32_t apt = LdsAddr(in_pt) + 32 * lane;
       const uint32_t aid = LdsAddr(in_ids) + 4 * lane;
       cse_v4i c0 = LdsRead128<0>(acam), c1 = LdsRead128<16>(acam), c2 = LdsRead128<32>(acam);
       cse_v4i c3 = LdsRead128<48>(acam), c4 = LdsRead128<64>(acam);
       cse_v4i ob = LdsRead128<0>(aobs);
-      double p0 = LdsRead64<0>(apt), p1 = LdsRead64<8>(apt), p2 = LdsRead64<16>(apt);
+      // x = bytes 0..7, y = 8..11 | 16..19, z = 20..27 (4-byte aligned).
+      double p0 = LdsRead64<0>(apt);
+      int y0 = LdsRead32<8>(apt), y1 = LdsRead32<16>(apt);
+      int z0 = LdsRead32<20>(apt), z1 = LdsRead32<24>(apt);
       int i0 = LdsRead32<0>(aid), i1 = LdsRead32<4 * kWave>(aid);
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4)
                    : : "memory");
-      asm volatile("" : "+v"(ob), "+v"(p0), "+v"(p1), "+v"(p2), "+v"(i0), "+v"(i1));
+      asm volatile("" : "+v"(ob), "+v"(p0), "+v"(y0), "+v"(y1), "+v"(z0), "+v"(z1), "+v"(i0),
+                   "+v"(i1));
+      const double p1 = __builtin_bit_cast(double, ((uint64_t)(uint32_t)y1 << 32) | (uint32_t)y0);
+      const double p2 = __builtin_bit_cast(double, ((uint64_t)(uint32_t)z1 << 32) | (uint32_t)z0);
       double cam[10];
       V4iToDoubles(c0, cam);
       V4iToDoubles(c1, cam + 2);
@@ -1414,6 +1422,285 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
   }
   if (failed_any && lane == 0) StoreB32(a.status, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave ends
+}
+
+// ---------------------------------------------------------------------------
+// EvaluateAffineStream: persistent, one wave per workgroup, every input of
+// chunk c + W fetched by LDS-DMA while chunk c computes (as
+// EvaluateAffinePipelined), built around two gfx950 behaviours that stall
+// a persistent wave (tools/membench2.hip, tools/ldsdma_probe.hip):
+//   * a vector-memory instruction reads its VGPR operands (address and
+//     store data) when it reaches the head of the CU's memory queue, which
+//     under the write stream is thousands of cycles after issue; rewriting
+//     such a register first stalls the wave until then.  So the DMA address
+//     registers of chunk c + W stay live until the wait that retires those
+//     DMAs (top of the next chunk), the stores take their data from one of
+//     kSets rotating accumulation-register sets (AgprSet<k>, loaded straight
+//     from the LDS staging buffer), and their addresses are a constant lane
+//     offset plus wave-uniform SGPR bases.
+//   * the DMA of 12-byte pieces leaves a 4-byte hole per lane.
+// BSM Snavely<2,9,3> with residuals and Jacobian requested (the headline
+// workload); other shapes take EvaluateAffineChunks.
+// ---------------------------------------------------------------------------
+#include "agpr_sets.inc"
+
+__device__ __forceinline__ uint64_t Uniform64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+struct StreamDma {
+  const void* cam[5];
+  const void* obs;
+  const void* pt[2];
+  const void* ids[2];
+};
+
+__device__ __forceinline__ void StreamIssueIds(const GroupArgs& a, int64_t cc, int lane, int32_t* ids,
+                                               StreamDma* d) {
+  const int32_t* src = a.ids + 2 * PipeBlock(a, cc, lane);
+  d->ids[0] = src;
+  d->ids[1] = src + 1;
+  __builtin_amdgcn_global_load_lds(src, ids, 4, 0, 2);
+  __builtin_amdgcn_global_load_lds(src + 1, ids + kWave, 4, 0, 2);
+}
+
+__device__ __forceinline__ void StreamIssueGather(const GroupArgs& a, int64_t cc, int lane, int2 id,
+                                                  double* cam, double* obs, double* pt,
+                                                  StreamDma* d) {
+  constexpr int kPieces = 5;  // Snavely camera: 10 doubles in the packed table
+  const int cid_own = id.x - a.packed0_lo;
+#pragma unroll
+  for (int k = 0; k < kPieces; ++k) {
+    const int p = k * kWave + lane;
+    const int t = p / kPieces, q = p - t * kPieces;
+    const int cid = __shfl(cid_own, t, kWave);
+    const double* src = a.packed0 + (int64_t)10 * cid + 2 * q;
+    d->cam[k] = src;
+    __builtin_amdgcn_global_load_lds(src, cam + 2 * kWave * k, 16, 0, 0);
+  }
+  const double* so = a.data + 2 * PipeBlock(a, cc, lane);
+  d->obs = so;
+  __builtin_amdgcn_global_load_lds(so, obs, 16, 0, 2);
+  const double* base = a.state + a.state_base[1];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = k * kWave + lane;
+    const int pid = __shfl(id.y, p >> 1, kWave);
+    const char* src = reinterpret_cast<const char*>(base + 3 * (int64_t)pid) + 12 * (p & 1);
+    d->pt[k] = src;
+    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<char*>(pt) + 16 * kWave * k, 12, 0, 2);
+  }
+}
+
+// The previous DMA batch has landed (the caller waited): its address
+// registers may be rewritten from here on.
+__device__ __forceinline__ void StreamRelease(const StreamDma& d) {
+  asm volatile("" ::"v"(d.cam[0]), "v"(d.cam[1]), "v"(d.cam[2]), "v"(d.cam[3]), "v"(d.cam[4]),
+               "v"(d.obs), "v"(d.pt[0]), "v"(d.pt[1]), "v"(d.ids[0]), "v"(d.ids[1]));
+}
+
+struct StreamLds {
+  double* cam;
+  double* obs;
+  double* pt;
+  int32_t* ids;
+  double* stage;
+};
+
+struct StreamState {
+  int64_t c;
+  int2 idc;
+  StreamDma dma;
+  bool first;
+  bool failed;
+  uint32_t voff;   // 16 * lane: the store offset of every piece
+  uint32_t voff2;  // 16 * lane + 5120
+  uint32_t vzero;  // 0: the partial's offset
+};
+
+// One chunk with store set kSet.  Returns false when the wave is done.
+// kSplit: stage F, pull it into the set, then stage E in the same LDS
+// (9 instead of 12 KiB of staging per wave).
+template <class K, int kLoss, int kSet, bool kSplit = false>
+__device__ __forceinline__ bool StreamStep(const GroupArgs& a, StreamState& S, const StreamLds& L,
+                                           int lane, int64_t nchunks, int64_t W) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  constexpr int kStores = 14;  // 13 pieces + the partial, per full chunk
+  if (S.c >= nchunks) return false;
+  // Everything but the previous chunk's stores has landed, in issue order.
+  if (S.first)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kStores) : "memory");
+  S.first = false;
+  StreamRelease(S.dma);
+  __builtin_amdgcn_wave_barrier();
+  AffineInputs<K> in;
+  in.id0 = S.idc.x;
+  in.id1 = S.idc.y;
+  int2 idn;
+  {
+    const uint32_t acam = LdsAddr(L.cam) + 80 * lane;
+    const uint32_t aobs = LdsAddr(L.obs) + 16 * lane;
+    const uint32_t apt = LdsAddr(L.pt) + 32 * lane;
+    const uint32_t aid = LdsAddr(L.ids) + 4 * lane;
+    cse_v4i c0 = LdsRead128<0>(acam), c1 = LdsRead128<16>(acam), c2 = LdsRead128<32>(acam);
+    cse_v4i c3 = LdsRead128<48>(acam), c4 = LdsRead128<64>(acam);
+    cse_v4i ob = LdsRead128<0>(aobs);
+    double p0 = LdsRead64<0>(apt);
+    int y0 = LdsRead32<8>(apt), y1 = LdsRead32<16>(apt);
+    int z0 = LdsRead32<20>(apt), z1 = LdsRead32<24>(apt);
+    int i0 = LdsRead32<0>(aid), i1 = LdsRead32<4 * kWave>(aid);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4)
+                 : : "memory");
+    asm volatile("" : "+v"(ob), "+v"(p0), "+v"(y0), "+v"(y1), "+v"(z0), "+v"(z1), "+v"(i0),
+                 "+v"(i1));
+    double cam[10];
+    V4iToDoubles(c0, cam);
+    V4iToDoubles(c1, cam + 2);
+    V4iToDoubles(c2, cam + 4);
+    V4iToDoubles(c3, cam + 6);
+    V4iToDoubles(c4, cam + 8);
+#pragma unroll
+    for (int k = 0; k < S0; ++k) in.x0[k] = cam[k];
+    V4iToDoubles(ob, in.d);
+    in.x1[0] = p0;
+    in.x1[1] = __builtin_bit_cast(double, ((uint64_t)(uint32_t)y1 << 32) | (uint32_t)y0);
+    in.x1[2] = __builtin_bit_cast(double, ((uint64_t)(uint32_t)z1 << 32) | (uint32_t)z0);
+    idn = make_int2(i0, i1);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // Next chunk's inputs (clamped past the end: harmless re-reads).
+  const int64_t c = S.c;
+  const int64_t cn = c + W < nchunks ? c + W : nchunks - 1;
+  const int64_t cnn = c + 2 * W < nchunks ? c + 2 * W : nchunks - 1;
+  StreamIssueGather(a, cn, lane, idn, L.cam, L.obs, L.pt, &S.dma);
+  StreamIssueIds(a, cnn, lane, L.ids, &S.dma);
+
+  const int64_t i0 = c * kWave;
+  const int64_t rem = a.n - i0;
+  const int nw = rem < kWave ? (int)rem : kWave;
+  const bool active = lane < nw;
+  double r[NR], J0[NR * S0], J1[NR * S1p];
+  bool ok = EvaluateFunctor<K, true>(in.d, in.x0, in.x1, r, J0, J1);
+  if (ok && a.check_finite) {
+    const bool bad = AnyNonFinite<NR>(r) || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
+    ok = !bad;
+  }
+  const double cost = LossAndCorrect<K, kLoss, true>(a.loss, a.apply_loss, r, J0, J1);
+  double wsum = active ? cost : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
+  S.failed = S.failed || (__ballot(active && !ok) != 0);
+  S.c = c + W;
+  S.idc = idn;
+
+  if (!FastTail<K, true, false>(a, i0, nw)) {
+    // The group's last, partial chunk: the generic staged stores.
+    // (Also every chunk when an output is not requested.)  The next step
+    // waits for everything: its store count is not kStores.
+    StageAndStore<K, true, false, true, true>(a, L.stage, lane, active, i0, nw, r, J0, J1);
+    if (lane == 0) StoreB64(a.partials + c, wsum);
+    S.first = true;
+    return true;
+  }
+  // Stage the E and F cells (lane-major, as EvaluateAffineChunks), then
+  // pull them into the store set as 16-byte pieces in segment order.
+  double* st = L.stage;
+  double* st1 = kSplit ? st : st + kWave * NR * S0;
+#pragma unroll
+  for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
+  if constexpr (kSplit) {
+    __builtin_amdgcn_wave_barrier();
+    AgprSet<kSet>::LoadStageF(LdsAddr(st) + 16 * lane);  // waits for its reads
+    __builtin_amdgcn_wave_barrier();
+  }
+#pragma unroll
+  for (int k = 0; k < NR; ++k)
+#pragma unroll
+    for (int cc = 0; cc < S1; ++cc) st1[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (kSplit)
+    AgprSet<kSet>::LoadStageE(LdsAddr(st) + 16 * lane);
+  else
+    AgprSet<kSet>::LoadStage(LdsAddr(st) + 16 * lane);
+  AgprSet<kSet>::PutRes(r[0], r[1], wsum);
+  // Wave-uniform bases, forced into SGPRs (the "s" constraint alone lets
+  // the compiler hand a VGPR pair to the assembler here).
+  const uint64_t f0 = Uniform64(reinterpret_cast<uint64_t>(a.jacobian + a.jac_base[0][0] +
+                                                           a.jac_stride[0] * i0));
+  const uint64_t e0 = Uniform64(reinterpret_cast<uint64_t>(a.jacobian + a.jac_base[1][0] +
+                                                           a.jac_stride[1] * i0));
+  const uint64_t r0 = Uniform64(reinterpret_cast<uint64_t>(a.residuals + a.res_base + (int64_t)NR * i0));
+  const uint64_t p0 = Uniform64(reinterpret_cast<uint64_t>(a.partials + c));
+  AgprSet<kSet>::StoreAll(S.voff, S.voff2, f0, e0, r0);
+  if (lane == 0) AgprSet<kSet>::StorePartial(S.vzero, p0);
+  // The staging buffer is rewritten by the next chunk only after these
+  // LDS reads (in-order LDS queue; StoreAll waited lgkmcnt(0) anyway).
+  return true;
+}
+
+template <class K, int kLoss, int kSets, bool kSplit>
+__device__ __forceinline__ void AffineStreamBody(const GroupArgs& a) {
+  using Tr = KindTraits<K>;
+  static_assert(Tr::NB == 2 && Tr::S0 == 9 && Tr::S1 == 3 && Tr::D == 2 && Tr::NR == 2,
+                "Snavely<2,9,3>-shaped groups only");
+  __shared__ double in_cam[kWave * 10];
+  __shared__ double in_obs[kWave * 2];
+  __shared__ double in_pt[4 * kWave];
+  __shared__ int32_t in_ids[2 * kWave];
+  __shared__ double stage[kWave * (kSplit ? 18 : 24)];
+  const StreamLds L{in_cam, in_obs, in_pt, in_ids, stage};
+
+  const int lane = threadIdx.x;
+  const int64_t nchunks = (a.n + kWave - 1) / kWave;
+  const int64_t W = gridDim.x;
+  StreamState S;
+  S.c = blockIdx.x;
+  if (S.c >= nchunks) return;
+  S.first = true;
+  S.failed = false;
+  S.voff = 16u * lane;
+  S.voff2 = 16u * lane + 5120u;
+  S.vzero = 0u;
+  asm volatile("" : "+v"(S.voff), "+v"(S.voff2), "+v"(S.vzero));
+  // Prologue: ids(c), then gather(c) and ids(c + W).
+  StreamIssueIds(a, S.c, lane, in_ids, &S.dma);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  S.idc = make_int2(in_ids[lane], in_ids[kWave + lane]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  StreamIssueGather(a, S.c, lane, S.idc, in_cam, in_obs, in_pt, &S.dma);
+  StreamIssueIds(a, S.c + W < nchunks ? S.c + W : nchunks - 1, lane, in_ids, &S.dma);
+  for (;;) {
+    if (!StreamStep<K, kLoss, 0, kSplit>(a, S, L, lane, nchunks, W)) break;
+    if constexpr (kSets > 1)
+      if (!StreamStep<K, kLoss, 1, kSplit>(a, S, L, lane, nchunks, W)) break;
+    if constexpr (kSets > 2)
+      if (!StreamStep<K, kLoss, 2, kSplit>(a, S, L, lane, nchunks, W)) break;
+    if constexpr (kSets > 3)
+      if (!StreamStep<K, kLoss, 3, kSplit>(a, S, L, lane, nchunks, W)) break;
+  }
+  if (S.failed && lane == 0) StoreB32(a.status, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the wave ends
+  asm volatile("" ::"v"(S.voff), "v"(S.voff2), "v"(S.vzero));
+}
+
+template <class K, int kLoss, int kSets>
+__global__ __launch_bounds__(kWave) void EvaluateAffineStream(const GroupArgs a) {
+  AffineStreamBody<K, kLoss, kSets, false>(a);
+}
+
+// Two waves per SIMD (256 registers per wave), two-round staging (17.5 KiB
+// of LDS per wave: 8 waves per CU fit).
+template <class K, int kLoss, int kSets>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+EvaluateAffineStream2(const GroupArgs a) {
+  AffineStreamBody<K, kLoss, kSets, true>(a);
 }
 
 // Diagnostic only: tools/membench2.hip's m1 memory path (camera gather
