@@ -184,6 +184,40 @@ void LaunchPipelined(const cse::GroupArgs& a, int64_t, hipStream_t s) {
                      dim3((unsigned)PipelinedGrid(a.n)), dim3(cse::kWave), 0, s, a);
 }
 
+// Residual-only and cost-only evaluations (no Jets): the same pipelined
+// persistent kernel at $CSE_VALUES_WAVES (default 16) waves per CU; its
+// registers and 9 KB of LDS per wave allow that many.
+int64_t ValuesGrid(int64_t n) {
+  static int per_cu = -1, cus = 256;
+  if (per_cu < 0) {
+    const char* e = getenv("CSE_VALUES_WAVES");
+    per_cu = e && atoi(e) > 0 ? atoi(e) : 16;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const int64_t chunks = (n + cse::kWave - 1) / cse::kWave;
+  return std::max<int64_t>(1, std::min<int64_t>(chunks, (int64_t)cus * per_cu));
+}
+
+template <class K, int L>
+void LaunchValuesPipelined(const cse::GroupArgs& a, int64_t, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffinePipelined<K, L, false, false>),
+                     dim3((unsigned)ValuesGrid(a.n)), dim3(cse::kWave), 0, s, a);
+}
+
+// $CSE_VALUES_VARIANT: 0 = one chunk per wave (EvaluateAffineChunks), 1 =
+// pipelined persistent (Snavely-shaped affine groups with the LDS-DMA
+// camera table).
+int ValuesVariant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CSE_VALUES_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 // The persistent stream kernel: one wave per workgroup, $CSE_STREAM_WAVES
 // (default 4: one per SIMD) waves per CU, at most one per chunk.
 int64_t StreamGrid(int64_t n) {
@@ -326,6 +360,14 @@ LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
     LaunchFn f = loss == CSE_LOSS_HUBER ? SnavelyVariant<cse::kLossHuber>(v)
                : loss == CSE_LOSS_TRIVIAL ? SnavelyVariant<cse::kLossTrivial>(v) : nullptr;
     if (f) return f;
+  }
+  if (!jac && dma && policy != kTable && ValuesVariant() == 1) {
+    // The residual layout is the same for both affine policies.
+    using SK = cse::SnavelyKind;  // the kernel's LDS image is Snavely-shaped
+    if (kind == CSE_FUNCTOR_SNAVELY_2_9_3)
+      return loss == CSE_LOSS_HUBER    ? &LaunchValuesPipelined<SK, cse::kLossHuber>
+           : loss == CSE_LOSS_CAUCHY ? &LaunchValuesPipelined<SK, cse::kLossCauchy>
+                                     : &LaunchValuesPipelined<SK, cse::kLossTrivial>;
   }
   switch (kind) {
     case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, policy, dma);

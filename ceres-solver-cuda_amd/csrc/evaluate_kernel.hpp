@@ -1262,13 +1262,18 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
   constexpr int kStores = kQ0 + kQ1 + 2;  // vector stores per full chunk (+ the partial)
   static_assert(kStores <= 63, "vmcnt field");
   const bool exact = a.residuals != nullptr && (!kJac || a.jacobian != nullptr);
+  // Cost-only (candidate) evaluations: the partial is the chunk's one store.
+  const bool cost_only = !kJac && a.residuals == nullptr;
 
   for (; c < nchunks; c += W) {
     // Everything issued before the previous chunk's kStores stores has
-    // landed (vmcnt counts in issue order).  Without both outputs the store
-    // count differs: wait for everything (correct, not pipelined).
-    if (first || !exact || !prev_fast)
+    // landed (vmcnt counts in issue order).  With other output sets the
+    // store count differs: the cost-only form waits for its one store, any
+    // other waits for everything (correct, not pipelined).
+    if (first || !prev_fast || !(exact || cost_only))
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (cost_only)
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kStores) : "memory");
     first = false;
@@ -1405,9 +1410,8 @@ __global__ __launch_bounds__(kWave) void EvaluateAffinePipelined(const GroupArgs
       }
     }
     asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
-    // Exactly kStores vector stores per full chunk for the wait at the top
-    // (the Jacobian-less and residual-less forms are not pipelined: host
-    // check).
+    // Exactly kStores vector stores per full chunk (one when cost-only) for
+    // the wait at the top.
     if (jac) {
       SegmentStoresFrom<0, kQ0>(f0, f1, q0);
       if constexpr (kQ1 > 0) SegmentStoresFrom<0, kQ1>(e0, e1, q1);
