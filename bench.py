@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--gradient", action="store_true", help="also produce the gradient J^T r")
+    ap.add_argument("--gradient-mode", type=int, default=0, choices=[0, 1, 2],
+                    help="cse_options.gradient_mode: 0 fused (default), 1 post-pass, 2 atomics")
     ap.add_argument("--mode", default="jacobian",
                     choices=["jacobian", "residual", "candidate", "spmv"],
                     help="jacobian: residual+Jacobian evaluation (the headline metric); "
@@ -151,7 +153,8 @@ def main():
     build_s = time.perf_counter() - t_build
 
     stream = torch.cuda.current_stream(dev)
-    ev = ca.Evaluator(prog, device=dev_index, profile=True, stream=stream.cuda_stream)
+    ev = ca.Evaluator(prog, device=dev_index, profile=True, stream=stream.cuda_stream,
+                      gradient_mode=args.gradient_mode)
     info = ev.info()
     f64 = torch.float64
     state = torch.from_numpy(prog.state).to(dev)

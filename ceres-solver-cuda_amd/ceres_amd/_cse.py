@@ -80,7 +80,8 @@ class cse_problem_desc(C.Structure):
 class cse_options(C.Structure):
     _fields_ = [("device", C.c_int32), ("check_finite", C.c_int32),
                 ("apply_loss_function", C.c_int32), ("force_general_layout", C.c_int32),
-                ("profile", C.c_int32), ("use_stream", C.c_int32), ("stream", C.c_void_p)]
+                ("profile", C.c_int32), ("use_stream", C.c_int32), ("stream", C.c_void_p),
+                ("gradient_mode", C.c_int32)]
 
 
 class cse_info(C.Structure):
@@ -88,7 +89,7 @@ class cse_info(C.Structure):
                 ("num_parameters", C.c_int64), ("num_effective_parameters", C.c_int64),
                 ("num_jacobian_values", C.c_int64), ("num_groups", C.c_int32),
                 ("num_affine_groups", C.c_int32), ("device", C.c_int32),
-                ("reserved", C.c_int32), ("bytes_jacobian_eval", C.c_int64),
+                ("num_fused_gradient_groups", C.c_int32), ("bytes_jacobian_eval", C.c_int64),
                 ("bytes_residual_eval", C.c_int64)]
 
 

@@ -111,6 +111,10 @@ def _synthetic(num_cameras, num_points, num_observations, seed, outlier_fraction
 
 def _distinct_rows(rng, n, k, C):
     """n rows of k distinct integers in [0, C)."""
+    if k * k > 4 * C:
+        # Dense rows (most of the cameras per point, test shapes only):
+        # rejection sampling would almost never draw k distinct values.
+        return np.argsort(rng.random((n, C)), axis=1)[:, :k].astype(np.int32)
     m = rng.integers(0, C, (n, k), dtype=np.int32)
     while True:
         s = np.sort(m, axis=1)

@@ -348,7 +348,7 @@ class Evaluator:
     """ProgramEvaluatorCUDA seam over libcse.so (program_evaluator_cuda.h:65-183)."""
 
     def __init__(self, program, device=-1, check_finite=True, apply_loss_function=True,
-                 force_general_layout=False, profile=False, stream=None):
+                 force_general_layout=False, profile=False, stream=None, gradient_mode=0):
         self.program = program
         self.desc = program.descriptor()
         opts = _cse.cse_options()
@@ -359,6 +359,8 @@ class Evaluator:
         opts.apply_loss_function = int(apply_loss_function)
         opts.force_general_layout = int(force_general_layout)
         opts.profile = int(profile)
+        # 0 = fused where eligible (else 1), 1 = post-pass, 2 = atomics (cse.h)
+        opts.gradient_mode = int(gradient_mode)
         # stream: a hipStream_t handle (int) to run on -- 0 is the null stream
         # (torch's default stream); None = an evaluator-owned stream.
         opts.use_stream = int(stream is not None)

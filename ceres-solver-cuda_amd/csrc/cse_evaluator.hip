@@ -118,6 +118,10 @@ struct Group {
     DevBuf<double> chunk_partial;
     int64_t nchunks = 0;
   } grad[2];
+  // Fused gradient (cse::FusedGrad): eligible groups, and their slot-1
+  // boundary entries and slot-0 contributions (allocated on first use).
+  bool fuse_ok = false;
+  DevBuf<double> gside, gcontrib;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -155,6 +159,23 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   }
   hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, Two, Dbg, WPB>),
                      dim3((unsigned)num_wg), dim3(cse::kWave * WPB), 0, s, a);
+}
+
+// The shipped kernel with the fused gradient (Snavely groups, gradient_mode 0).
+template <int L, bool Crs>
+void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunks<cse::SnavelyKind, L, true, Crs, 2, false, 0,
+                                                cse::kWavesPerBlock, true>),
+                     dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
+}
+
+LaunchFn PickFused(int loss, int policy) {
+  const bool crs = policy == 2;  // kAffineCrs
+  switch (loss) {
+    case CSE_LOSS_HUBER: return crs ? &LaunchFused<cse::kLossHuber, true> : &LaunchFused<cse::kLossHuber, false>;
+    case CSE_LOSS_CAUCHY: return crs ? &LaunchFused<cse::kLossCauchy, true> : &LaunchFused<cse::kLossCauchy, false>;
+    default: return crs ? &LaunchFused<cse::kLossTrivial, true> : &LaunchFused<cse::kLossTrivial, false>;
+  }
 }
 
 template <int kStep>
@@ -509,7 +530,8 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
   plan->lo = lo;
   plan->count = count;
   plan->wave = !sorted && n >= 32 * count;  // on average 32+ blocks per parameter block
-  if (plan->wave) {
+  // Chunks: the wave-mode post-pass and the fused gradient's slot-0 pass.
+  if (!sorted) {
     std::vector<int64_t> begin, coff(count + 1, 0);
     for (int64_t p = 0; p < count; ++p) {
       coff[p] = (int64_t)begin.size();
@@ -734,9 +756,20 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     // Gradient: a deterministic post-pass over the written residuals and
     // Jacobian when the group has plans for all its slots, else in-kernel
     // FP64 atomics (as the reference).
-    bool grad_pass = d_grad && d_res && d_jac && G.affine;
+    bool grad_pass = d_grad && d_res && d_jac && G.affine && ev->opts.gradient_mode != 2;
     for (int j = 0; j < G.shape.nb; ++j) grad_pass = grad_pass && G.grad[j].ready;
-    const cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
+    const bool fused = grad_pass && G.fuse_ok && ev->opts.gradient_mode == 0;
+    cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
+    if (fused) {
+      const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
+      int rc;
+      if ((rc = G.gside.ensure((size_t)(2 * chunks * 4)))) return rc;
+      if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
+      a.gfused = d_grad;
+      a.gside = G.gside.p;
+      a.gcontrib = G.gcontrib.p;
+      fn = PickFused(G.loss.kind, G.policy);
+    }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
       const int64_t total = G.slot0_count * G.slot0_stride;
@@ -746,7 +779,28 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
-    if (grad_pass) {
+    if (fused) {
+      const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
+      hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
+                         dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                         dim3(cse::kBlockThreads), 0, ev->stream, G.gside.p, entries, d_grad,
+                         G.delta_base[1]);
+      const Group::GradPlan& P = G.grad[0];
+      cse::GradArgs ga{};
+      ga.count = P.count;
+      ga.lo = P.lo;
+      ga.grad = d_grad;
+      ga.delta_base = G.delta_base[0];
+      const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
+      if (P.nchunks > 0)
+        hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
+                           dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
+                           dim3(cse::kBlockThreads), 0, ev->stream, G.gcontrib.p, P.perm.p, ch);
+      hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
+                         dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                         dim3(cse::kBlockThreads), 0, ev->stream, ga, ch);
+      CSE_HIP(hipGetLastError());
+    } else if (grad_pass) {
       const int sizes[2] = {G.shape.s0, G.shape.s1};
       for (int j = 0; j < G.shape.nb; ++j) {
         const Group::GradPlan& P = G.grad[j];
@@ -871,6 +925,8 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   // Groups.
   int64_t covered_res = 0, covered_jac = 0;
   std::vector<char> seen(d->num_parameter_blocks, 0);
+  // Which (group, slot) uses each parameter block: -1 none, -2 several.
+  std::vector<int32_t> owner(d->num_parameter_blocks, -1);
   for (int gi = 0; gi < d->num_groups; ++gi) {
     const cse_residual_group& g = d->groups[gi];
     Group G;
@@ -901,6 +957,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
         if (pb.size != want)
           return bail(Fail(CSE_ERR_INVALID, "parameter block size does not match the functor"));
         if (!pb.is_constant) covered_jac += (int64_t)k.nr * pb.tangent_size;
+        const int32_t tag = 2 * gi + j;
+        if (owner[id] == -1) owner[id] = tag;
+        else if (owner[id] != tag) owner[id] = -2;
         if (!seen[id]) {
           seen[id] = 1;
           ev->bytes_jac += 8LL * pb.size;
@@ -967,6 +1026,20 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     ev->groups.push_back(std::move(G));
   }
   ev->bytes_jac += 8LL * covered_jac;
+  // Fused gradient eligibility: a Snavely group on the affine LDS-DMA path
+  // whose slot-1 blocks are sorted (identity plan) and used by no other
+  // group or slot (the fused kernel stores their rows, it does not add),
+  // and whose slot-0 blocks have a chunked plan.
+  for (int gi = 0; gi < (int)ev->groups.size(); ++gi) {
+    Group& G = ev->groups[gi];
+    bool ok = G.kind == CSE_FUNCTOR_SNAVELY_2_9_3 && G.affine && G.n > 0 && G.packed0.p &&
+              G.grad[0].ready && G.grad[0].perm.p && G.grad[0].nchunks > 0 && G.grad[1].ready &&
+              G.grad[1].perm.p == nullptr;
+    const cse_residual_group& g = d->groups[gi];
+    for (int64_t i = 0; ok && i < g.num_blocks; ++i)
+      ok = owner[g.parameter_block_ids[2 * i + 1]] == 2 * gi + 1;
+    G.fuse_ok = ok;
+  }
   ev->res_covered = covered_res == d->num_residuals;
   ev->jac_covered = covered_jac == d->num_jacobian_values;
 
@@ -1264,7 +1337,10 @@ int cse_get_info(cse_evaluator* ev, cse_info* info) {
   info->num_effective_parameters = ev->num_effective;
   info->num_jacobian_values = ev->num_jacobian_values;
   info->num_groups = (int32_t)ev->groups.size();
-  for (auto& G : ev->groups) info->num_affine_groups += G.affine ? 1 : 0;
+  for (auto& G : ev->groups) {
+    info->num_affine_groups += G.affine ? 1 : 0;
+    info->num_fused_gradient_groups += (G.fuse_ok && ev->opts.gradient_mode == 0) ? 1 : 0;
+  }
   info->device = ev->device;
   info->bytes_jacobian_eval = ev->bytes_jac;
   info->bytes_residual_eval = ev->bytes_res;

@@ -84,6 +84,13 @@ struct GroupArgs {
   double* partials;
   int* status;
   uint64_t* timeline;  // diagnostics only ($CSE_TIMELINE): 8 u64 per wave, or null
+  // Fused gradient (EvaluateAffineChunks<..., kGradF = true>, see
+  // FusedGradient below): the gradient (delta offsets), the slot-1
+  // wave-boundary entries [2 * chunks][4] and the slot-0 per-block
+  // contributions J0^T r [n][S0p].
+  double* gfused;
+  double* gside;
+  double* gcontrib;
   LossParams loss;
   int apply_loss;
   int check_finite;
@@ -820,6 +827,94 @@ __device__ __forceinline__ int64_t PartialSlot(int64_t b, int64_t num_wg, int wa
   return ((b & 7) * per_xcd + (b >> 3)) * wpb + wave;
 }
 
+// One double at addr + kOff bytes, default cache policy (the fused
+// gradient's scattered slot-1 rows: neighbouring lanes share lines in L2).
+template <int kOff>
+__device__ __forceinline__ void StoreB64At(double* addr, double value) {
+  asm volatile("global_store_dwordx2 %0, %1, off offset:%2" ::"v"(addr), "v"(value), "i"(kOff)
+               : "memory");
+}
+
+// Segmented inclusive scan over the wave's lanes, fixed order (Hillis-
+// Steele).  Keys are non-decreasing across lanes, so key[l - off] == key[l]
+// means the whole range between is one run; afterwards each run's last lane
+// holds the run's sum.
+template <int S>
+__device__ __forceinline__ void SegmentedScan(double* v, int key, int lane) {
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int ku = __shfl_up(key, off, kWave);
+    double vu[S];
+#pragma unroll
+    for (int c = 0; c < S; ++c) vu[c] = __shfl_up(v[c], off, kWave);
+    if (lane >= off && ku == key) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) v[c] += vu[c];
+    }
+  }
+}
+
+// The fused gradient of one wave (EvaluateAffineChunks<..., kGradF>): the
+// deterministic replacement of the reference's in-kernel atomics
+// (cuda_evaluator_kernel.h:149-160, 189-217) for Schur-ordered groups.
+//   Slot 1 (points): the group's blocks are sorted by their slot-1 id, so a
+//   parameter block's blocks are one run of lanes.  SegmentedScan leaves
+//   the run's J1^T r in its last lane.  A run that touches neither end of
+//   the wave is this wave's alone: stored straight into the gradient (the
+//   host grants the group exclusive ownership of its slot-1 blocks).  The
+//   wave's first and last runs may continue in the neighbouring waves: they
+//   go to two boundary entries per wave (sum, id), which
+//   GradientBoundaryKernel adds up in wave order.  A one-run wave writes
+//   its run to entry 2c and a zero to entry 2c + 1 (same id).
+//   Slot 0 (cameras, random order): each block's J0^T r, padded to S0p
+//   doubles, in block order, for GradientContribKernel.
+template <class K>
+struct FusedGrad {
+  static constexpr int S0 = KindTraits<K>::S0, S1 = KindTraits<K>::S1;
+  static constexpr int S0p = (S0 + 1) & ~1;
+  double g0[S0p];
+  double g1[4];  // S1 == 3 sums, then the id (exact as a double)
+  bool interior = false, writer = false;
+  int64_t entry = 0;
+  int key = 0;
+
+  __device__ __forceinline__ void Compute(const double* r, const double* J0, const double* J1,
+                                          int id1, bool active, int lane, int nw, int64_t c) {
+    using Tr = KindTraits<K>;
+    constexpr int NR = Tr::NR, S1p = Tr::S1p;
+    static_assert(Tr::NB == 2 && S1 == 3, "fused gradient: two slots, the second of size 3");
+#pragma unroll
+    for (int cc = 0; cc < S0p; ++cc) {
+      double s = 0.0;
+      if (cc < S0) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) s += J0[k * S0 + cc] * r[k];
+      }
+      g0[cc] = s;
+    }
+#pragma unroll
+    for (int cc = 0; cc < S1; ++cc) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < NR; ++k) s += J1[k * S1p + cc] * r[k];
+      g1[cc] = active ? s : 0.0;
+    }
+    key = active ? id1 : 0x7fffffff;
+    SegmentedScan<S1>(g1, key, lane);
+    const int knext = __shfl_down(key, 1, kWave);
+    const bool run_end = lane == nw - 1 || (lane < nw - 1 && knext != key);
+    const int k0 = __shfl(key, 0, kWave);
+    const int kl = __shfl(key, nw - 1, kWave);
+    const bool single = k0 == kl;
+    const bool zero_entry = single && lane == 0 && nw > 1;
+    interior = active && run_end && key != k0 && key != kl;
+    writer = active && ((run_end && key == k0) || lane == nw - 1 || zero_entry);
+    entry = 2 * c + (single ? (zero_entry ? 1 : 0) : (lane == nw - 1 ? 1 : 0));
+    if (zero_entry) g1[0] = g1[1] = g1[2] = 0.0;
+    g1[3] = (double)key;
+  }
+};
+
 template <int kCount>
 __device__ __forceinline__ void KeepAlive(const cse_v4i* q) {
 #pragma unroll
@@ -865,7 +960,7 @@ __device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw)
 // 2 skips every output store (compute floor), 4 skips the LDS transpose
 // (each lane stores its own values at the coalesced positions).
 template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = false,
-          int kDebug = 0, int kWPB = kWavesPerBlock>
+          int kDebug = 0, int kWPB = kWavesPerBlock, bool kGradF = false>
 __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = Tr::N;
@@ -967,6 +1062,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
   const bool failed = __ballot(active && !ok) != 0;
   int* status_dst = a.status;
+  static_assert(!kGradF || (kJac && kDebug == 0), "fused gradient: real Jacobian kernels only");
+  FusedGrad<K> fg;
+  if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
   if constexpr ((kDebug & 2) != 0) {
     if (lane == 0) *partial_dst = wsum;
@@ -975,6 +1073,30 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if (!FastTail<K, kJac, kCrs>(a, i0, nw)) {
     if constexpr ((kDebug & 12) == 0)
       StageAndStore<K, kJac, kCrs, true, !kTwoRound>(a, st, lane, active, i0, nw, r, J0, J1);
+    if constexpr (kGradF) {
+      // The group's last, partial chunk: plain stores.
+      constexpr int S0p = FusedGrad<K>::S0p;
+      if (active) {
+        double* cdst = a.gcontrib + (int64_t)S0p * (i0 + lane);
+#pragma unroll
+        for (int cc = 0; cc < S0p; ++cc) cdst[cc] = fg.g0[cc];
+      }
+      if (fg.interior) {
+        double* g = a.gfused + a.delta_base[1] + 3LL * fg.key;
+        g[0] = fg.g1[0];
+        g[1] = fg.g1[1];
+        g[2] = fg.g1[2];
+      }
+      if (fg.writer) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a.gside[4 * fg.entry + q] = fg.g1[q];
+      }
+      if (nw == 1 && lane == 0) {  // a one-block wave: its zero entry
+        double* e = a.gside + 4 * (2 * c + 1);
+        e[0] = e[1] = e[2] = 0.0;
+        e[3] = fg.g1[3];
+      }
+    }
     if (lane == 0) {
       *partial_dst = wsum;
       if (failed) *status_dst = 1;
@@ -1078,6 +1200,30 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       }
     }
   }
+  // Fused gradient: the slot-0 contributions staged through the same LDS
+  // (after the Jacobian pieces have been read back), the slot-1 entry.
+  constexpr int kGQ = kGradF ? FusedGrad<K>::S0p / 2 : 1;
+  static_assert(kGQ <= 8, "contribution pieces: one base register");
+  cse_v4i gq[kGQ], sq[2];
+  double *cb0 = nullptr, *gp = nullptr, *sp = nullptr;
+  if constexpr (kGradF) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < kGQ; ++j)
+      reinterpret_cast<double2*>(st)[lane * kGQ + j] = make_double2(fg.g0[2 * j], fg.g0[2 * j + 1]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < kGQ; ++j) {
+      const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
+      gq[j] = AsV4i(v.x, v.y);
+    }
+    sq[0] = AsV4i(fg.g1[0], fg.g1[1]);
+    sq[1] = AsV4i(fg.g1[2], fg.g1[3]);
+    cb0 = a.gcontrib + (int64_t)(2 * kGQ) * i0 + 2 * lane + 512;
+    gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
+    sp = a.gside + 4 * fg.entry;
+  }
   // Residual pieces: the lane's own NR doubles (NR even).
   constexpr int kQr = NR / 2;
   cse_v4i qr[kQr];
@@ -1122,6 +1268,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kQr >= 2) StoreNt16<16, kPol>(rdst, qr[1]);
     if constexpr (kQr >= 3) StoreNt16<32, kPol>(rdst, qr[2]);
   }
+  if constexpr (kGradF) {
+    SegmentStoresFrom<0, kGQ>(cb0, cb0, gq);
+    if (fg.interior) {
+      StoreB64At<0>(gp, fg.g1[0]);
+      StoreB64At<8>(gp, fg.g1[1]);
+      StoreB64At<16>(gp, fg.g1[2]);
+    }
+    if (fg.writer) {
+      StoreNt16<0, 1>(sp, sq[0]);
+      StoreNt16<16, 1>(sp, sq[1]);
+    }
+  }
   // The cost partial (one per wave, lane 0) and the failure flag, last.
   if (lane == 0) {
     if (!kPartFirst && (kDebug & 32768) == 0) StoreB64<kPartPol>(v_partial, v_wsum);
@@ -1143,6 +1301,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
   KeepAlive<kQr>(qr);
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(v_partial), "v"(v_wsum));
+  if constexpr (kGradF) {
+    KeepAlive<kGQ>(gq);
+    KeepAlive<2>(sq);
+    asm volatile("" ::"v"(cb0), "v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1798,9 +1961,9 @@ __global__ __launch_bounds__(kBlockThreads) void MembenchM1Kernel(const GroupArg
 }
 
 template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = false,
-          int kDebug = 0, int kWPB = kWavesPerBlock>
+          int kDebug = 0, int kWPB = kWavesPerBlock, bool kGradF = false>
 __global__ __launch_bounds__(kWave * kWPB) void EvaluateAffineChunks(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug, kWPB>(a);
+  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug, kWPB, kGradF>(a);
 }
 
 // The general (table) path; also runs affine groups when
@@ -2077,6 +2240,66 @@ __global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const
   double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
 #pragma unroll
   for (int c = 0; c < S; ++c) dst[c] += acc[c];
+}
+
+// Fused-gradient slot 0 (FusedGrad): each chunk of a parameter block's
+// block list sums the blocks' written contributions (S of the SP doubles
+// per block; two 64-byte sectors per block instead of the Jacobian cell
+// and residual pair), a fixed butterfly, then GradientChunkReduceKernel.
+template <int S, int SP>
+__global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const double* contrib,
+                                                                       const int32_t* perm,
+                                                                       const GradChunks ch) {
+  static_assert(SP % 2 == 0 && SP >= S, "16-byte records");
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (cid >= ch.nchunks) return;
+  const int64_t q1 = ch.begin[cid + 1];
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
+    const double2* rec = reinterpret_cast<const double2*>(contrib + (int64_t)SP * perm[q]);
+#pragma unroll
+    for (int h = 0; h < SP / 2; ++h) {
+      const double2 v = rec[h];
+      if (2 * h < S) acc[2 * h] += v.x;
+      if (2 * h + 1 < S) acc[2 * h + 1] += v.y;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < S; ++c)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < S; ++c) ch.partial[cid * S + c] = acc[c];
+  }
+}
+
+// Fused-gradient slot 1: the waves' boundary entries (sum[S], id) are in
+// wave order, so their ids are non-decreasing; the first entry of each id
+// adds that id's entries in order and stores the row (the evaluation owns
+// these rows exclusively: no interior run of any wave wrote them).
+template <int S>
+__global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const double* side,
+                                                                        int64_t count,
+                                                                        double* grad,
+                                                                        int64_t delta_base) {
+  static_assert(S <= 3, "entries hold 3 sums and the id");
+  const int64_t e = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (e >= count) return;
+  const double key = side[4 * e + 3];
+  if (e > 0 && side[4 * (e - 1) + 3] == key) return;
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t f = e; f < count && side[4 * f + 3] == key; ++f)
+#pragma unroll
+    for (int c = 0; c < S; ++c) acc[c] += side[4 * f + c];
+  double* dst = grad + delta_base + (int64_t)S * (int64_t)key;
+#pragma unroll
+  for (int c = 0; c < S; ++c) dst[c] = acc[c];
 }
 
 // Identity order (the points of a Schur-ordered problem): one 64-thread

@@ -145,6 +145,13 @@ typedef struct cse_options {
   int32_t use_stream;           /* 1: run on `stream` as given, even NULL (the null stream) */
   void* stream;                 /* hipStream_t to run on; NULL and use_stream 0 =
                                    an evaluator-owned stream */
+  int32_t gradient_mode;        /* how g = J^T r is summed when the residuals and
+                                   Jacobian are requested too: 0 (default) = fused
+                                   into the evaluation where eligible, else 1;
+                                   1 = a fixed-order post-pass over the written
+                                   Jacobian; 2 = in-kernel FP64 atomics, as
+                                   cuda_evaluator_kernel.h:149-160.  0 and 1 are
+                                   bit-deterministic. */
 } cse_options;
 
 typedef struct cse_evaluator cse_evaluator;
@@ -232,7 +239,8 @@ typedef struct cse_info {
   int32_t num_groups;
   int32_t num_affine_groups;  /* groups on the table-free fast path */
   int32_t device;
-  int32_t reserved;
+  int32_t num_fused_gradient_groups; /* groups whose gradient is fused into the
+                                        evaluation (options.gradient_mode 0) */
   /* Compulsory HBM bytes of one residual+Jacobian evaluation (SURVEY.md
    * §8(d)): per block functor data + parameter ids + residuals + Jacobian
    * values, plus each distinct parameter block read once. */

@@ -46,7 +46,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_cse.cse_loss) == 24
     assert ctypes.sizeof(_cse.cse_parameter_block) == 40
     assert ctypes.sizeof(_cse.cse_residual_group) == 72
-    assert ctypes.sizeof(_cse.cse_options) == 32
+    assert ctypes.sizeof(_cse.cse_options) == 40
 
 
 def test_create_rejects_bad_descriptors_without_a_gpu():
