@@ -164,8 +164,7 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 // The shipped kernel with the fused gradient (Snavely groups, gradient_mode 0).
 template <int L, bool Crs>
 void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunks<cse::SnavelyKind, L, true, Crs, 2, false, 0,
-                                                cse::kWavesPerBlock, true>),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<cse::SnavelyKind, L, Crs>),
                      dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
 }
 
@@ -336,6 +335,8 @@ LaunchFn SnavelyVariant(int v) {
     case 56: return &LaunchStream<K, L, 1>;  // 1 set (the register hazard kept: A/B)
     case 57: return &LaunchStream2<K, L, 2>;  // 2 waves per SIMD, 2 sets, two-round staging
     case 58: return &LaunchStream2<K, L, 1>;  // 2 waves per SIMD, 1 set
+    case 59: return &LaunchChunks<K, L, true, false, 2, false, 131072>;  // XCD-contiguous chunks
+    case 60: return &LaunchChunks<K, L, true, false, 2, false, 262144>;  // chunk-interleaved XCDs
     default: return nullptr;
   }
 }

@@ -976,7 +976,25 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
-  const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
+  // kDebug bit 131072 (tuning variant): XCD-contiguous chunk ranges --
+  // workgroups are dealt round-robin over the 8 XCDs, so XCD x runs
+  // workgroups x, x + 8, ...; remapped, XCD x walks one contiguous range.
+  int64_t bid = blockIdx.x;
+  if constexpr ((kDebug & 131072) != 0) {
+    const int64_t per = (gridDim.x + 7) / 8;
+    const int64_t x = bid & 7, k = bid >> 3;
+    const int64_t full = gridDim.x - (per - 1) * 8;  // XCDs that get `per` workgroups
+    bid = x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
+  }
+  int64_t c = bid * kWPB + wave;
+  // kDebug bit 262144 (tuning variant): the 8 workgroups dispatched
+  // together (one per XCD) interleave their chunks one by one instead of
+  // taking kWPB consecutive chunks each.
+  if constexpr ((kDebug & 262144) != 0) {
+    const int64_t grp = bid >> 3, x = bid & 7;
+    c = (grp * kWPB + wave) * 8 + x;
+    if ((grp + 1) * 8 > gridDim.x) c = bid * kWPB + wave;  // the ragged last group: identity
+  }
   double* partial_dst =
       a.partials + ((kDebug & 65536) ? PartialSlot(blockIdx.x, gridDim.x, wave, kWPB) : c);
   if (c >= num_chunks) {
@@ -1964,6 +1982,15 @@ template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = 
           int kDebug = 0, int kWPB = kWavesPerBlock, bool kGradF = false>
 __global__ __launch_bounds__(kWave * kWPB) void EvaluateAffineChunks(const GroupArgs a) {
   AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug, kWPB, kGradF>(a);
+}
+
+// The fused-gradient form of the shipped kernel, held to 3 waves per SIMD
+// (168 VGPRs): the LDS bound of 3 workgroups per CU.  Unbounded, the CRS
+// form takes 170 VGPRs and drops to 2.
+template <class K, int kLoss, bool kCrs>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(3))) void
+EvaluateAffineChunksFused(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, true, kCrs, 2, false, 0, kWavesPerBlock, true>(a);
 }
 
 // The general (table) path; also runs affine groups when
