@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--gradient-mode", type=int, default=0, choices=[0, 1, 2],
                     help="cse_options.gradient_mode: 0 fused (default), 1 post-pass, 2 atomics")
     ap.add_argument("--mode", default="jacobian",
-                    choices=["jacobian", "residual", "candidate", "spmv"],
+                    choices=["jacobian", "residual", "candidate", "spmv", "cgnr"],
                     help="jacobian: residual+Jacobian evaluation (the headline metric); "
                          "residual: residuals+cost only; candidate: the trust-region candidate "
                          "step, Plus(x, delta) then cost-only evaluation "
@@ -167,9 +167,10 @@ def main():
     if args.mode == "candidate":
         delta = torch.full((prog.num_effective_parameters,), 1e-6, dtype=f64, device=dev)
         cand = torch.empty_like(state)
-    if args.mode == "spmv":
+    if args.mode in ("spmv", "cgnr"):
         ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None, jac.data_ptr())
         pvec = torch.ones(prog.num_effective_parameters, dtype=f64, device=dev)
+        dvec = torch.full((prog.num_effective_parameters,), 0.5, dtype=f64, device=dev)
         jp = torch.zeros(prog.num_residuals, dtype=f64, device=dev)
         jtjp = torch.zeros(prog.num_effective_parameters, dtype=f64, device=dev)
 
@@ -182,6 +183,10 @@ def main():
         elif args.mode == "candidate":
             ev.plus_device(state.data_ptr(), delta.data_ptr(), cand.data_ptr())
             ev.evaluate_device(cand.data_ptr(), cost.data_ptr(), None, None, None)
+        elif args.mode == "cgnr":  # one pass: J^T J p + D^2 p (cse_cgnr_multiply)
+            ev.cgnr_multiply_device(jac.data_ptr(), dvec.data_ptr(), pvec.data_ptr(),
+                                    jtjp.data_ptr())
+            return
         else:
             ev.right_multiply_device(jac.data_ptr(), pvec.data_ptr(), jp.data_ptr())
             ev.left_multiply_device(jac.data_ptr(), jp.data_ptr(), jtjp.data_ptr())
@@ -208,7 +213,7 @@ def main():
     status = ev.wait()
     last_ms, total_ms, launches = ev.kernel_stats()
     kernel_ms = total_ms / max(launches, 1)
-    if args.mode == "spmv":  # no evaluate launches in the timed loop: the step time
+    if args.mode in ("spmv", "cgnr"):  # no evaluate launches in the timed loop: the step time
         kernel_ms = elapsed / args.steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=f64, device=dev)
@@ -268,6 +273,9 @@ def main():
         # J read twice, p/J p/J^T J p vectors; kernel_ms (events around the
         # evaluate launches only) does not apply, the step time does
         bytes_per_launch = 2 * 8 * prog.num_jacobian_values
+    elif args.mode == "cgnr":
+        # the normal operator's compulsory bytes: J once, p, D and y
+        bytes_per_launch = 8 * prog.num_jacobian_values + 4 * 8 * prog.num_effective_parameters
     elif args.mode == "candidate":
         # the timed kernel is the cost-only evaluation (no residual stores);
         # Plus is in ms_per_step, not in kernel_ms_avg
@@ -307,7 +315,8 @@ def main():
                             f"{args.loss} {args.format} "
                             + {"jacobian": "residual+Jacobian", "residual": "residual+cost",
                                "candidate": "Plus + cost-only",
-                               "spmv": "J p + J^T (J p)"}[args.mode]
+                               "spmv": "J p + J^T (J p)",
+                               "cgnr": "J^T J p + D^2 p (one pass)"}[args.mode]
                             + f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
                 "blocks_per_rank": shard_info["blocks"],

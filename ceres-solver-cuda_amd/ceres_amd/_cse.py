@@ -112,6 +112,7 @@ SIGNATURES = {
     "cse_plus": (C.c_int, [C.c_void_p, P_f64, P_f64, P_f64]),
     "cse_jacobian_right_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_jacobian_left_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_cgnr_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_destroy": (None, [C.c_void_p]),
     "cse_last_error": (C.c_char_p, []),
     "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),

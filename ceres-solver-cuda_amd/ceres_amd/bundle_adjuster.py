@@ -108,11 +108,12 @@ def solve(args):
                            jac.data_ptr())
         return ev.wait()
 
-    def normal_op(v, lam_d):
-        Jv = torch.zeros(m, dtype=f64, device=dev)
-        ev.right_multiply_device(jac.data_ptr(), v.data_ptr(), Jv.data_ptr())
-        out = lam_d * v
-        ev.left_multiply_device(jac.data_ptr(), Jv.data_ptr(), out.data_ptr())
+    def normal_op(v, sqrt_lam_d):
+        # (J^T J + lam D) v in one pass over J (cse_cgnr_multiply, the
+        # CudaCgnrLinearOperator of cgnr_solver.cc:226-237).
+        out = torch.zeros(n, dtype=f64, device=dev)
+        ev.cgnr_multiply_device(jac.data_ptr(), sqrt_lam_d.data_ptr(), v.data_ptr(),
+                                out.data_ptr())
         return out
 
     def cgnr(lam):
@@ -120,7 +121,7 @@ def solve(args):
         # equations (cgnr_solver.cc), D = diag(J^T J).
         b = -g
         Minv = 1.0 / ((1.0 + lam) * D)
-        lam_d = lam * D
+        sqrt_lam_d = torch.sqrt(lam * D)
         dx = torch.zeros(n, dtype=f64, device=dev)
         res = b.clone()
         z = Minv * res
@@ -129,7 +130,7 @@ def solve(args):
         bn = b.norm()
         it = 0
         for it in range(1, args.max_linear_solver_iterations + 1):
-            Ap = normal_op(p, lam_d)
+            Ap = normal_op(p, sqrt_lam_d)
             alpha = rz / torch.dot(p, Ap)
             dx += alpha * p
             res -= alpha * Ap

@@ -426,6 +426,12 @@ class Evaluator:
         return _cse.check(_cse.lib().cse_jacobian_left_multiply(self.handle, d_jacobian, d_x, d_y),
                           "cse_jacobian_left_multiply")
 
+    def cgnr_multiply_device(self, d_jacobian, d_D, d_x, d_y):
+        """y += J^T (J x) + D.*D.*x on the device, d_D may be None
+        (CudaCgnrLinearOperator::RightMultiplyAndAccumulate, cgnr_solver.cc:226-237)."""
+        return _cse.check(_cse.lib().cse_cgnr_multiply(self.handle, d_jacobian, d_D, d_x, d_y),
+                          "cse_cgnr_multiply")
+
     def plus_device(self, d_state, d_delta, d_out):
         """Device-pointer Plus on the evaluator's stream.  Async."""
         return _cse.check(_cse.lib().cse_plus_device(self.handle, d_state, d_delta, d_out),

@@ -453,6 +453,7 @@ struct cse_evaluator {
   DevBuf<int> status;  // [0] running flag, [1] last status
   // Host-path buffers (allocated on first use).
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
+  DevBuf<double> cg_z;  // cse_cgnr_multiply's z = J x when it cannot fuse
   int* status_host = nullptr;  // pinned
   // Profiling: one (start, stop) event pair per evaluation around its
   // group kernels, folded lazily so timing never stalls the launch queue.
@@ -722,6 +723,32 @@ int FoldTiming(cse_evaluator* ev) {
   return CSE_OK;
 }
 
+// After a fused kernel (the evaluator's FusedGrad or CgnrMultiplyKernel):
+// add the slot-1 boundary entries and the slot-0 contributions, per
+// parameter block in a fixed order, into out (delta offsets).
+int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
+  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
+  hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
+                     dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
+  const Group::GradPlan& P = G.grad[0];
+  cse::GradArgs ga{};
+  ga.count = P.count;
+  ga.lo = P.lo;
+  ga.grad = out;
+  ga.delta_base = G.delta_base[0];
+  const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
+  if (P.nchunks > 0)
+    hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
+                       dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
+                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch);
+  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
+                     dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, ga, ch);
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
 // Enqueue one evaluation on ev->stream.
 int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_res,
             double* d_grad, double* d_jac) {
@@ -781,26 +808,8 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
     if (fused) {
-      const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
-      hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
-                         dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                         dim3(cse::kBlockThreads), 0, ev->stream, G.gside.p, entries, d_grad,
-                         G.delta_base[1]);
-      const Group::GradPlan& P = G.grad[0];
-      cse::GradArgs ga{};
-      ga.count = P.count;
-      ga.lo = P.lo;
-      ga.grad = d_grad;
-      ga.delta_base = G.delta_base[0];
-      const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
-      if (P.nchunks > 0)
-        hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
-                           dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
-                           dim3(cse::kBlockThreads), 0, ev->stream, G.gcontrib.p, P.perm.p, ch);
-      hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
-                         dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                         dim3(cse::kBlockThreads), 0, ev->stream, ga, ch);
-      CSE_HIP(hipGetLastError());
+      const int rc = LaunchFusedGradTail(G, d_grad, ev->stream);
+      if (rc) return rc;
     } else if (grad_pass) {
       const int sizes[2] = {G.shape.s0, G.shape.s1};
       for (int j = 0; j < G.shape.nb; ++j) {
@@ -1244,6 +1253,50 @@ int cse_jacobian_right_multiply(cse_evaluator* ev, const double* d_jacobian_valu
 int cse_jacobian_left_multiply(cse_evaluator* ev, const double* d_jacobian_values,
                                const double* d_x, double* d_y) {
   return JacobianMultiply(ev, d_jacobian_values, d_x, d_y, true);
+}
+
+int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                      const double* d_x, double* d_y) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (!ev->has_layout) return Fail(CSE_ERR_INVALID, "the descriptor had no Jacobian layout");
+  if (!d_jacobian_values || !d_x || !d_y) return Fail(CSE_ERR_INVALID, "null pointer");
+  CSE_HIP(hipSetDevice(ev->device));
+  hipStream_t s = ev->stream;
+  if (d_D && ev->num_effective > 0)
+    hipLaunchKernelGGL(cse::DtDxpyKernel,
+                       dim3((unsigned)((ev->num_effective + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                       dim3(cse::kBlockThreads), 0, s, d_D, d_x, d_y, ev->num_effective);
+  bool fused = true;
+  for (auto& G : ev->groups) fused = fused && (G.n == 0 || G.fuse_ok);
+  if (!fused) {
+    // z = J x, then y += J^T z: the two products of CudaCgnrLinearOperator.
+    int rc;
+    if ((rc = ev->cg_z.ensure((size_t)std::max<int64_t>(ev->num_residuals, 1)))) return rc;
+    CSE_HIP(hipMemsetAsync(ev->cg_z.p, 0, ev->num_residuals * sizeof(double), s));
+    if ((rc = JacobianMultiply(ev, d_jacobian_values, d_x, ev->cg_z.p, false))) return rc;
+    return JacobianMultiply(ev, d_jacobian_values, ev->cg_z.p, d_y, true);
+  }
+  for (auto& G : ev->groups) {
+    if (G.n == 0) continue;
+    const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
+    int rc;
+    if ((rc = G.gside.ensure((size_t)(2 * chunks * 4)))) return rc;
+    if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
+    cse::GroupArgs a = MakeArgs(ev, G, nullptr, nullptr, const_cast<double*>(d_jacobian_values),
+                                nullptr);
+    a.gside = G.gside.p;
+    a.gcontrib = G.gcontrib.p;
+    const dim3 grid((unsigned)((chunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
+    if (G.policy == kAffineCrs)
+      hipLaunchKernelGGL((cse::CgnrMultiplyKernel<cse::SnavelyKind, true>), grid,
+                         dim3(cse::kBlockThreads), 0, s, a, d_x, d_y);
+    else
+      hipLaunchKernelGGL((cse::CgnrMultiplyKernel<cse::SnavelyKind, false>), grid,
+                         dim3(cse::kBlockThreads), 0, s, a, d_x, d_y);
+    CSE_HIP(hipGetLastError());
+    if ((rc = LaunchFusedGradTail(G, d_y, s))) return rc;
+  }
+  return CSE_OK;
 }
 
 int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_delta,

@@ -2306,8 +2306,8 @@ __global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const dou
 
 // Fused-gradient slot 1: the waves' boundary entries (sum[S], id) are in
 // wave order, so their ids are non-decreasing; the first entry of each id
-// adds that id's entries in order and stores the row (the evaluation owns
-// these rows exclusively: no interior run of any wave wrote them).
+// adds that id's entries in order and adds the sum to the row (no interior
+// run of any wave touched these rows).
 template <int S>
 __global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const double* side,
                                                                         int64_t count,
@@ -2326,7 +2326,7 @@ __global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const do
     for (int c = 0; c < S; ++c) acc[c] += side[4 * f + c];
   double* dst = grad + delta_base + (int64_t)S * (int64_t)key;
 #pragma unroll
-  for (int c = 0; c < S; ++c) dst[c] = acc[c];
+  for (int c = 0; c < S; ++c) dst[c] += acc[c];
 }
 
 // Identity order (the points of a Schur-ordered problem): one 64-thread
@@ -2456,6 +2456,155 @@ __global__ __launch_bounds__(kBlockThreads) void MultiplyTableKernel(const Group
 #pragma unroll
     for (int k = 0; k < NR; ++k) y[res + k] += acc[k];
   }
+}
+
+// The CGNR normal operator in one pass over J (cse_cgnr_multiply):
+// y += J^T (J x), replacing CudaCgnrLinearOperator::RightMultiplyAndAccumulate
+// (internal/ceres/cgnr_solver.cc:226-237), which runs z = J x and y += J^T z
+// as two sparse products (two reads of J and a round trip of z).  One wave
+// per 64-block chunk, as the evaluator:
+//   * the wave's Jacobian image (BSM: its F then E segments; CRS: its rows)
+//     comes in by LDS-DMA, 1 KiB per instruction, and each lane reads its
+//     block's cells from LDS;
+//   * z_b = J_b x (two values) stays in registers;
+//   * slot 1 (points): E_b^T z_b through the fused gradient's segmented
+//     scan -- interior runs add into y directly, the wave's first and last
+//     runs go to boundary entries (GradientBoundaryKernel adds them);
+//   * slot 0 (cameras): F_b^T z_b in block order (GradientContribKernel and
+//     GradientChunkReduceKernel add them per camera, fixed order).
+// Deterministic; the host requires the fused gradient's eligibility.
+template <class K, bool kCrs>
+__global__ __launch_bounds__(kBlockThreads) void CgnrMultiplyKernel(const GroupArgs a,
+                                                                    const double* x, double* y) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, N = Tr::N;
+  static_assert(Tr::NB == 2 && NR == 2 && S1 == 3, "Snavely-shaped groups");
+  constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kImg = kWave * NR * N;        // doubles of one wave's Jacobian image
+  constexpr int kPieces = kImg / (2 * kWave);  // 16-byte DMA pieces per lane
+  static_assert(kImg % (2 * kWave) == 0 && (kWave * NR * S0) % (2 * kWave) == 0, "16-B pieces");
+  __shared__ double img[kWavesPerBlock][kImg];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t nchunks = (a.n + kWave - 1) / kWave;
+  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (c >= nchunks) return;
+  double* im = img[wave];
+  const int64_t i0 = c * kWave;
+  const int nw = a.n - i0 < kWave ? (int)(a.n - i0) : kWave;
+  const bool active = lane < nw;
+  const int64_t i = active ? i0 + lane : a.n - 1;
+  const long long idw = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
+  const int id0 = (int)idw, id1 = (int)(idw >> 32);
+
+  // Column c of row k of slot j for this lane's block, at LDS offset
+  // off[j][k] + c (full chunks) -- or straight from HBM (the last chunk).
+  const int64_t row0 = kCrs ? (a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0]
+                                                                     : a.jac_base[1][0])
+                            : 0;
+  double F[NR * S0], E[NR * S1];
+  if (nw == kWave) {
+    if constexpr (kCrs) {
+      const double* seg = a.jacobian + row0 + (int64_t)NR * N * i0;
+#pragma unroll
+      for (int k = 0; k < kPieces; ++k)
+        __builtin_amdgcn_global_load_lds(seg + 2 * (k * kWave + lane), im + 2 * kWave * k, 16, 0, 0);
+    } else {
+      const double* segF = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+      const double* segE = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+      constexpr int kF = kWave * NR * S0 / (2 * kWave);
+#pragma unroll
+      for (int k = 0; k < kF; ++k)
+        __builtin_amdgcn_global_load_lds(segF + 2 * (k * kWave + lane), im + 2 * kWave * k, 16, 0, 0);
+#pragma unroll
+      for (int k = 0; k < kPieces - kF; ++k)
+        __builtin_amdgcn_global_load_lds(segE + 2 * (k * kWave + lane), im + 2 * kWave * (kF + k),
+                                         16, 0, 0);
+    }
+  }
+  double xc[S0], xp[S1];
+  {
+    const double* x0 = x + a.delta_base[0] + (int64_t)S0 * id0;
+    const double* x1 = x + a.delta_base[1] + (int64_t)S1 * id1;
+#pragma unroll
+    for (int k = 0; k < S0; ++k) xc[k] = x0[k];
+#pragma unroll
+    for (int k = 0; k < S1; ++k) xp[k] = x1[k];
+  }
+  if (nw == kWave) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int f0 = kCrs ? (int)(a.jac_base[0][k] - row0) + NR * N * lane : NR * S0 * lane + S0 * k;
+      const int e0 = kCrs ? (int)(a.jac_base[1][k] - row0) + NR * N * lane
+                          : kWave * NR * S0 + NR * S1 * lane + S1 * k;
+#pragma unroll
+      for (int cc = 0; cc < S0; ++cc) F[k * S0 + cc] = im[f0 + cc];
+#pragma unroll
+      for (int cc = 0; cc < S1; ++cc) E[k * S1 + cc] = im[e0 + cc];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double* rf = a.jacobian + a.jac_base[0][k] + a.jac_stride[0] * i;
+      const double* re = a.jacobian + a.jac_base[1][k] + a.jac_stride[1] * i;
+#pragma unroll
+      for (int cc = 0; cc < S0; ++cc) F[k * S0 + cc] = rf[cc];
+#pragma unroll
+      for (int cc = 0; cc < S1; ++cc) E[k * S1 + cc] = re[cc];
+    }
+  }
+  double z[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    double t = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < S0; ++cc) t += F[k * S0 + cc] * xc[cc];
+#pragma unroll
+    for (int cc = 0; cc < S1; ++cc) t += E[k * S1 + cc] * xp[cc];
+    z[k] = active ? t : 0.0;
+  }
+  // J_b^T z_b: FusedGrad with z in place of r (its J1 rows are S1p = S1 wide).
+  FusedGrad<K> fg;
+  fg.Compute(z, F, E, id1, active, lane, nw, c);
+  if (fg.interior) {
+    double* row = y + a.delta_base[1] + (int64_t)S1 * fg.key;
+    row[0] += fg.g1[0];
+    row[1] += fg.g1[1];
+    row[2] += fg.g1[2];
+  }
+  if (fg.writer) {
+    double4* e = reinterpret_cast<double4*>(a.gside + 4 * fg.entry);
+    *e = make_double4(fg.g1[0], fg.g1[1], fg.g1[2], fg.g1[3]);
+  }
+  if (nw == 1 && lane == 0)
+    *reinterpret_cast<double4*>(a.gside + 4 * (2 * c + 1)) = make_double4(0.0, 0.0, 0.0, fg.g1[3]);
+  if (nw == kWave) {
+    // Camera contributions: staged (the image has been read), 16-B pieces.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < S0p / 2; ++j)
+      reinterpret_cast<double2*>(im)[lane * (S0p / 2) + j] = make_double2(fg.g0[2 * j], fg.g0[2 * j + 1]);
+    __builtin_amdgcn_wave_barrier();
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    v2d* dst = reinterpret_cast<v2d*>(a.gcontrib + (int64_t)S0p * i0);
+#pragma unroll
+    for (int j = 0; j < S0p / 2; ++j)
+      __builtin_nontemporal_store(reinterpret_cast<const v2d*>(im)[j * kWave + lane],
+                                  dst + j * kWave + lane);
+  } else if (active) {
+    double* dst = a.gcontrib + (int64_t)S0p * i;
+#pragma unroll
+    for (int cc = 0; cc < S0p; ++cc) dst[cc] = fg.g0[cc];
+  }
+}
+
+// y += D .* D .* x (CudaVector::DtDxpy, cgnr_solver.cc:236).
+__global__ __launch_bounds__(kBlockThreads) void DtDxpyKernel(const double* D, const double* x,
+                                                              double* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (i < n) y[i] += D[i] * D[i] * x[i];
 }
 
 // Program::Plus for manifold-free blocks: runs of consecutive state entries

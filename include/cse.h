@@ -225,6 +225,16 @@ int cse_jacobian_right_multiply(cse_evaluator* ev, const double* d_jacobian_valu
 int cse_jacobian_left_multiply(cse_evaluator* ev, const double* d_jacobian_values,
                                const double* d_x, double* d_y);
 
+/* The CGNR normal operator: y += J^T (J x) + D .* D .* x (d_D may be NULL),
+ * device pointers, asynchronous on the evaluator's stream.  Replaces
+ * CudaCgnrLinearOperator::RightMultiplyAndAccumulate
+ * (internal/ceres/cgnr_solver.cc:226-237: z = A x, y += A^T z, y.DtDxpy(D, x)).
+ * Groups eligible for the fused gradient (cse_info.num_fused_gradient_groups)
+ * read J once and never materialise z; otherwise the two products above.
+ * Deterministic on the affine path. */
+int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                      const double* d_x, double* d_y);
+
 void cse_destroy(cse_evaluator* ev);
 
 /* Thread-local description of the last error. */
