@@ -383,6 +383,23 @@ LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
                : loss == CSE_LOSS_TRIVIAL ? SnavelyVariant<cse::kLossTrivial>(v) : nullptr;
     if (f) return f;
   }
+  if (!jac && policy != kTable && ValuesVariant() >= 2 && ValuesVariant() <= 4 &&
+      kind == CSE_FUNCTOR_SNAVELY_2_9_3) {
+    // Tuning variants of the Jet-free kernel's camera gather: 2 = 8-byte
+    // pieces from the state, 3 = 16-byte register pieces from the repacked
+    // table (needs dma), 4 = per-lane loads.
+    using SK = cse::SnavelyKind;
+    const int v = ValuesVariant();
+    if (v == 3 && !dma) return nullptr;
+    const bool crs = policy == kAffineCrs;
+#define CSE_VV(L)                                                                    \
+  (v == 2 ? (crs ? &LaunchChunks<SK, L, false, true, 1> : &LaunchChunks<SK, L, false, false, 1>) \
+   : v == 3 ? (crs ? &LaunchChunks<SK, L, false, true, 3> : &LaunchChunks<SK, L, false, false, 3>) \
+            : (crs ? &LaunchChunks<SK, L, false, true, 0> : &LaunchChunks<SK, L, false, false, 0>))
+    return loss == CSE_LOSS_HUBER ? CSE_VV(cse::kLossHuber)
+         : loss == CSE_LOSS_CAUCHY ? CSE_VV(cse::kLossCauchy) : CSE_VV(cse::kLossTrivial);
+#undef CSE_VV
+  }
   if (!jac && dma && policy != kTable && ValuesVariant() == 1) {
     // The residual layout is the same for both affine policies.
     using SK = cse::SnavelyKind;  // the kernel's LDS image is Snavely-shaped
