@@ -177,6 +177,12 @@ LaunchFn PickFused(int loss, int policy) {
   }
 }
 
+template <class K, int L, int Dbg>
+void LaunchW3(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksW3<K, L, Dbg>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
+}
+
 template <int kStep>
 void LaunchM1(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   hipLaunchKernelGGL(cse::MembenchM1Kernel<kStep>, dim3((unsigned)num_wg),
@@ -337,6 +343,7 @@ LaunchFn SnavelyVariant(int v) {
     case 58: return &LaunchStream2<K, L, 1>;  // 2 waves per SIMD, 1 set
     case 59: return &LaunchChunks<K, L, true, false, 2, false, 131072>;  // XCD-contiguous chunks
     case 60: return &LaunchChunks<K, L, true, false, 2, false, 262144>;  // chunk-interleaved XCDs
+    case 61: return &LaunchW3<K, L, 524288>;  // twice the FP64 work, 3 waves/SIMD
     default: return nullptr;
   }
 }

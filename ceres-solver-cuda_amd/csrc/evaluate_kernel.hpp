@@ -1051,12 +1051,32 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   } else {
     ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
   }
+  // kDebug bit 524288 (diagnostic): the functor evaluated a second time on
+  // inputs the compiler cannot prove equal, its outputs folded in times an
+  // opaque zero -- twice the FP64 work, the same results.
+  double extra = 0.0;
+  if constexpr ((kDebug & 524288) != 0) {
+    double zero = 0.0;
+    asm volatile("" : "+v"(zero));
+    AffineInputs<K> in2 = in;
+    in2.x1[0] += zero * r[0];
+    double r2[NR], J02[NR * S0], J12[NR * S1p];
+    EvaluateFunctor<K, kJac>(in2.d, in2.x0, in2.x1, r2, J02, J12);
+    double s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) s2 += r2[k];
+#pragma unroll
+    for (int q = 0; q < NR * S0; ++q) s2 += J02[q];
+#pragma unroll
+    for (int q = 0; q < NR * S1p; ++q) s2 += J12[q];
+    extra = zero * s2;
+  }
   if (ok && a.check_finite) {
     bool bad = AnyNonFinite<NR>(r);
     if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
     ok = !bad;
   }
-  double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+  double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1) + extra;
   if constexpr ((kDebug & 2) != 0) {
 #pragma unroll
     for (int q = 0; q < NR * S0; ++q) cost += J0[q];
@@ -1982,6 +2002,13 @@ template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kTwoRound = 
           int kDebug = 0, int kWPB = kWavesPerBlock, bool kGradF = false>
 __global__ __launch_bounds__(kWave * kWPB) void EvaluateAffineChunks(const GroupArgs a) {
   AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, kTwoRound, kDebug, kWPB, kGradF>(a);
+}
+
+// Diagnostic variants held to 3 waves per SIMD (the shipped kernel's).
+template <class K, int kLoss, int kDebug>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(3))) void
+EvaluateAffineChunksW3(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, true, false, 2, false, kDebug>(a);
 }
 
 // The fused-gradient form of the shipped kernel, held to 3 waves per SIMD
