@@ -2,7 +2,9 @@
 
 The library is loaded from ceres-solver-cuda_amd/lib/libcse.so (built by
 `make` in ceres-solver-cuda_amd/ or __graft_entry__.build()).  There is no
-fallback: if the library is missing, loading raises.
+fallback: if the library is missing, loading raises.  use_library() selects
+another build of the same ABI before the first load (bench.py --lib tuning:
+lib/libcse_tuning.so, the A/B build of tools/).
 """
 import ctypes as C
 import os
@@ -23,6 +25,15 @@ SNAVELY_2_9_3 = 0
 SNAVELY_NO_DISTORTION_2_7_3 = 1
 SNAVELY_QUATERNION_2_10_3 = 2
 POINT_DISPLACEMENT_3_3 = 3
+# Known-answer-test functors of the reference's own tests (cse.h).
+TEST_LINEAR_3_2_3_4 = 100
+TEST_LINEAR_3_4_3_2 = 101
+TEST_LINEAR_2_2_3 = 102
+TEST_LINEAR_3_2_4 = 103
+TEST_LINEAR_4_3_4 = 104
+TEST_BILINEAR_1_2_2 = 110
+TEST_TEN_PARAMETER_1_x10 = 111
+TEST_PARTIAL_OUTPUT_2_1 = 112
 
 # (num_residuals, parameter block sizes, functor data size)
 FUNCTOR_SHAPES = {
@@ -30,6 +41,14 @@ FUNCTOR_SHAPES = {
     SNAVELY_NO_DISTORTION_2_7_3: (2, (7, 3), 2),
     SNAVELY_QUATERNION_2_10_3: (2, (10, 3), 2),
     POINT_DISPLACEMENT_3_3: (3, (3,), 3),
+    TEST_LINEAR_3_2_3_4: (3, (2, 3, 4), 2),
+    TEST_LINEAR_3_4_3_2: (3, (4, 3, 2), 2),
+    TEST_LINEAR_2_2_3: (2, (2, 3), 2),
+    TEST_LINEAR_3_2_4: (3, (2, 4), 2),
+    TEST_LINEAR_4_3_4: (4, (3, 4), 2),
+    TEST_BILINEAR_1_2_2: (1, (2, 2), 1),
+    TEST_TEN_PARAMETER_1_x10: (1, (1,) * 10, 1),
+    TEST_PARTIAL_OUTPUT_2_1: (2, (1,), 1),
 }
 
 # cse_loss_kind
@@ -128,6 +147,15 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+def use_library(path):
+    """Load `path` (a build of the same ABI) instead of lib/libcse.so.  Must
+    be called before the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libcse already loaded from " + LIB_PATH)
+    LIB_PATH = os.path.abspath(path)
 
 
 def lib():

@@ -5,6 +5,11 @@
 // picks a layout policy per residual group, and runs one fused kernel per
 // group plus one finalize kernel per evaluation
 // (RegisteredCUDAEvaluators::Evaluate, :46-103).
+//
+// The product library reads no environment variable: every kernel it can
+// launch is the shipped one for its (functor, loss, outputs, layout).  The
+// tuning build (make tuning, -DCSE_TUNING, tools/ only) adds alternative
+// settings of the hot kernel selected by $CSE_TUNE_VARIANT.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -13,10 +18,11 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/cse.h"
-#include "evaluate_kernel.hpp"
+#include "operator_kernels.hpp"
 
 namespace {
 
@@ -34,25 +40,75 @@ int Fail(int code, const std::string& msg) {
       return Fail(CSE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-struct KindShape {
-  int nr, nb, s0, s1, data;
-};
+// The functor kinds the library is built for.  Visit(kind, f) calls
+// f(K{}) with the kind's functor type; returns false for an unknown kind.
+using TestLinear3_234 = cse::LinearTestKind<3, 2, 3, 4>;
+using TestLinear3_432 = cse::LinearTestKind<3, 4, 3, 2>;
+using TestLinear2_23 = cse::LinearTestKind<2, 2, 3>;
+using TestLinear3_24 = cse::LinearTestKind<3, 2, 4>;
+using TestLinear4_34 = cse::LinearTestKind<4, 3, 4>;
 
-bool ShapeOf(int kind, KindShape* k) {
+template <class F>
+bool VisitKind(int kind, F&& f) {
   switch (kind) {
-    case CSE_FUNCTOR_SNAVELY_2_9_3: *k = {2, 2, 9, 3, 2}; return true;
-    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3: *k = {2, 2, 7, 3, 2}; return true;
-    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3: *k = {2, 2, 10, 3, 2}; return true;
-    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3: *k = {3, 1, 3, 0, 3}; return true;
+    case CSE_FUNCTOR_SNAVELY_2_9_3: f(cse::SnavelyKind{}); return true;
+    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3: f(cse::SnavelyNoDistortionKind{}); return true;
+    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3: f(cse::SnavelyQuaternionKind{}); return true;
+    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3: f(cse::PointDisplacementKind{}); return true;
+    case CSE_FUNCTOR_TEST_LINEAR_3_2_3_4: f(TestLinear3_234{}); return true;
+    case CSE_FUNCTOR_TEST_LINEAR_3_4_3_2: f(TestLinear3_432{}); return true;
+    case CSE_FUNCTOR_TEST_LINEAR_2_2_3: f(TestLinear2_23{}); return true;
+    case CSE_FUNCTOR_TEST_LINEAR_3_2_4: f(TestLinear3_24{}); return true;
+    case CSE_FUNCTOR_TEST_LINEAR_4_3_4: f(TestLinear4_34{}); return true;
+    case CSE_FUNCTOR_TEST_BILINEAR_1_2_2: f(cse::BilinearTestKind{}); return true;
+    case CSE_FUNCTOR_TEST_TEN_PARAMETER_1_x10: f(cse::TenParameterTestKind{}); return true;
+    case CSE_FUNCTOR_TEST_PARTIAL_OUTPUT_2_1: f(cse::PartialOutputTestKind{}); return true;
     default: return false;
   }
 }
 
+// Known-answer-test kinds: general path and trivial loss only.
+bool IsTestKind(int kind) { return kind >= 100; }
+
+struct KindShape {
+  int nr = 0, nb = 0, data = 0;
+  int sz[cse::kMaxSlots] = {};
+  int s0 = 0, s1 = 0;  // sz[0], sz[1] (0 if absent): the two-slot affine path
+};
+
+bool ShapeOf(int kind, KindShape* k) {
+  return VisitKind(kind, [&](auto kd) {
+    using K = decltype(kd);
+    using Tr = cse::KindTraits<K>;
+    k->nr = Tr::NR;
+    k->nb = Tr::NB;
+    k->data = Tr::D;
+    for (int j = 0; j < Tr::NB; ++j) k->sz[j] = K::kSizes[j];
+    k->s0 = k->sz[0];
+    k->s1 = Tr::NB > 1 ? k->sz[1] : 0;
+  });
+}
+
+// Device buffer, move-only, freed on destruction.
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr, o.n = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p, n = o.n;
+      o.p = nullptr, o.n = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }
   int alloc(size_t count) {
+    release();
     if (count == 0) return CSE_OK;
     if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
       p = nullptr;
@@ -64,7 +120,6 @@ struct DevBuf {
   // Allocate on first use / grow; keeps the buffer when large enough.
   int ensure(size_t count) {
     if (p && n >= count) return CSE_OK;
-    release();
     return alloc(count);
   }
   int upload(const T* h, size_t count, hipStream_t s) {
@@ -126,42 +181,29 @@ struct Group {
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
 
-// Cost reduction: above this many per-workgroup partials, a first pass of
+// Cost reduction: above this many per-wave partials, a first pass of
 // kPartialBlocks workgroups shortens the serial tail of FinalizeKernel.
 constexpr int64_t kPartialsTwoPass = 4096;
 constexpr int kPartialBlocks = 128;
 
+// Layout policy of a group: 0 = table, 1 = affine packed cells (BSM),
+// 2 = affine interleaved rows (CRS).
+enum Policy { kTable = 0, kAffinePacked = 1, kAffineCrs = 2 };
+
 template <class K, int L, bool J>
-void LaunchGeneral(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateGroupKernel<K, L, J>), dim3((unsigned)num_wg),
+void LaunchTable(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateTableKernel<K, L, J>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
-template <class K, int L, bool J, bool Crs, int Pf = -1, bool St = true, int Mw = 0, int Dbg = 4,
-          int Co = 2>
-void LaunchAffine(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  if constexpr (Mw == 0) {
-    hipLaunchKernelGGL((cse::EvaluateAffinePersistentD<K, L, J, Crs, Pf, St, Dbg, Co>),
-                       dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((cse::EvaluateAffinePersistent<K, L, J, Crs, Pf, St, Mw>),
-                       dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
-  }
-}
-
-// The shipped affine kernel: one chunk per wave, back-to-back store tail.
-template <class K, int L, bool J, bool Crs, int Co, bool Two = false, int Dbg = 0,
-          int WPB = cse::kWavesPerBlock>
+// The affine kernel: one 64-block chunk per wave, 4 waves per workgroup.
+template <class K, int L, bool J, bool Crs, int Co, class T = cse::ShippedTune>
 void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  if constexpr (WPB != cse::kWavesPerBlock) {
-    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-    num_wg = std::max<int64_t>(1, (chunks + WPB - 1) / WPB);
-  }
-  hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, Two, Dbg, WPB>),
-                     dim3((unsigned)num_wg), dim3(cse::kWave * WPB), 0, s, a);
+  hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, T>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
 }
 
-// The shipped kernel with the fused gradient (Snavely groups, gradient_mode 0).
+// The affine kernel with the fused gradient (Snavely groups, gradient_mode 0).
 template <int L, bool Crs>
 void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<cse::SnavelyKind, L, Crs>),
@@ -169,193 +211,13 @@ void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 LaunchFn PickFused(int loss, int policy) {
-  const bool crs = policy == 2;  // kAffineCrs
+  const bool crs = policy == kAffineCrs;
   switch (loss) {
     case CSE_LOSS_HUBER: return crs ? &LaunchFused<cse::kLossHuber, true> : &LaunchFused<cse::kLossHuber, false>;
     case CSE_LOSS_CAUCHY: return crs ? &LaunchFused<cse::kLossCauchy, true> : &LaunchFused<cse::kLossCauchy, false>;
     default: return crs ? &LaunchFused<cse::kLossTrivial, true> : &LaunchFused<cse::kLossTrivial, false>;
   }
 }
-
-template <class K, int L, int Dbg>
-void LaunchW3(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksW3<K, L, Dbg>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
-}
-
-template <int kStep>
-void LaunchM1(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL(cse::MembenchM1Kernel<kStep>, dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
-}
-
-// The software-pipelined persistent kernel: one wave per workgroup,
-// $CSE_PIPE_WAVES (default 8) waves per CU, at most one per chunk.
-int64_t PipelinedGrid(int64_t n) {
-  static int per_cu = -1, cus = 256;
-  if (per_cu < 0) {
-    const char* e = getenv("CSE_PIPE_WAVES");
-    per_cu = e && atoi(e) > 0 ? atoi(e) : 8;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  }
-  const int64_t chunks = (n + cse::kWave - 1) / cse::kWave;
-  return std::max<int64_t>(1, std::min<int64_t>(chunks, (int64_t)cus * per_cu));
-}
-
-template <class K, int L, bool J, bool Crs>
-void LaunchPipelined(const cse::GroupArgs& a, int64_t, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffinePipelined<K, L, J, Crs>),
-                     dim3((unsigned)PipelinedGrid(a.n)), dim3(cse::kWave), 0, s, a);
-}
-
-// Residual-only and cost-only evaluations (no Jets): the same pipelined
-// persistent kernel at $CSE_VALUES_WAVES (default 16) waves per CU; its
-// registers and 9 KB of LDS per wave allow that many.
-int64_t ValuesGrid(int64_t n) {
-  static int per_cu = -1, cus = 256;
-  if (per_cu < 0) {
-    const char* e = getenv("CSE_VALUES_WAVES");
-    per_cu = e && atoi(e) > 0 ? atoi(e) : 16;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  }
-  const int64_t chunks = (n + cse::kWave - 1) / cse::kWave;
-  return std::max<int64_t>(1, std::min<int64_t>(chunks, (int64_t)cus * per_cu));
-}
-
-template <class K, int L>
-void LaunchValuesPipelined(const cse::GroupArgs& a, int64_t, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffinePipelined<K, L, false, false>),
-                     dim3((unsigned)ValuesGrid(a.n)), dim3(cse::kWave), 0, s, a);
-}
-
-// $CSE_VALUES_VARIANT: 0 = one chunk per wave (EvaluateAffineChunks), 1 =
-// pipelined persistent (Snavely-shaped affine groups with the LDS-DMA
-// camera table).
-int ValuesVariant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CSE_VALUES_VARIANT");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-// The persistent stream kernel: one wave per workgroup, $CSE_STREAM_WAVES
-// (default 4: one per SIMD) waves per CU, at most one per chunk.
-int64_t StreamGrid(int64_t n) {
-  static int per_cu = -1, cus = 256;
-  if (per_cu < 0) {
-    const char* e = getenv("CSE_STREAM_WAVES");
-    per_cu = e && atoi(e) > 0 ? atoi(e) : 4;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  }
-  const int64_t chunks = (n + cse::kWave - 1) / cse::kWave;
-  return std::max<int64_t>(1, std::min<int64_t>(chunks, (int64_t)cus * per_cu));
-}
-
-template <class K, int L, int kSets>
-void LaunchStream(const cse::GroupArgs& a, int64_t, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineStream<K, L, kSets>), dim3((unsigned)StreamGrid(a.n)),
-                     dim3(cse::kWave), 0, s, a);
-}
-
-template <class K, int L, int kSets>
-void LaunchStream2(const cse::GroupArgs& a, int64_t, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineStream2<K, L, kSets>), dim3((unsigned)StreamGrid(a.n)),
-                     dim3(cse::kWave), 0, s, a);
-}
-
-// Tuning variants of the hot kernel (Snavely, Huber/Trivial, BSM,
-// Jacobian), selected by $CSE_AFFINE_VARIANT: (prefetch, LDS staging,
-// min waves per SIMD).
-template <int L>
-LaunchFn SnavelyVariant(int v) {
-  using K = cse::SnavelyKind;
-  switch (v) {
-    case 1: return &LaunchAffine<K, L, true, false, 2, true, 3, 0, 0>;
-    case 2: return &LaunchAffine<K, L, true, false, 1, true, 0, 0, 0>;
-    case 3: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, 0>;
-    case 4: return &LaunchAffine<K, L, true, false, 1, false, 0, 0, 0>;
-    case 5: return &LaunchAffine<K, L, true, false, 0, false, 0, 0, 0>;
-    case 6: return &LaunchAffine<K, L, true, false, 2, false, 0, 0, 0>;
-    case 7: return &LaunchAffine<K, L, true, false, 1, true, 4, 0, 0>;
-    case 8: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, 0>;
-    case 9: return &LaunchAffine<K, L, true, false, -1, false, 0, 0, 0>;
-    // Diagnostics (wrong results by design): memory floor, compute floor,
-    // plain (not non-temporal) stores.
-    case 10: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 0>;
-    case 11: return &LaunchAffine<K, L, true, false, -1, true, 0, 2, 0>;
-    case 12: return &LaunchAffine<K, L, true, false, -1, true, 0, 3, 0>;
-    case 13: return &LaunchAffine<K, L, true, false, -1, true, 0, 0, 1>;
-    case 14: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 1>;
-    case 15: return &LaunchAffine<K, L, true, false, 0, true, 0, 0, 1>;
-    case 16: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 1>;
-    case 17: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 2>;
-    case 18: return &LaunchAffine<K, L, true, false, -1, true, 0, 1, 2>;
-    case 19: return &LaunchAffine<K, L, true, false, -1, true, 0, 4, 2>;  // round-1 default
-    case 20: return &LaunchChunks<K, L, true, false, 2, true>;  // two-round staging
-    case 21: return &LaunchChunks<K, L, true, false, 2, false, 1>;  // memory floor
-    case 22: return &LaunchChunks<K, L, true, false, 2, false, 2>;  // compute floor
-    case 23: return &LaunchChunks<K, L, true, false, 2, false, 5>;  // memory floor, no transpose
-    case 24: return &LaunchChunks<K, L, true, false, 1, false, 1>;  // memory floor, register gather
-    case 25: return &LaunchChunks<K, L, true, false, 1, false, 5>;  // both
-    case 26: return &LaunchChunks<K, L, true, false, 2, false, 4>;  // real compute, no transpose
-    case 27: return &LaunchChunks<K, L, true, false, 2, false, 9>;  // memory floor, one data quad
-    case 28: return &LaunchChunks<K, L, true, false, 1, false, 9>;  // same, register gather
-    case 29: return &LaunchM1<0>;  // membench m1 memory path on the real buffers
-    case 30: return &LaunchM1<1>;  // + shipped store tail
-    case 31: return &LaunchM1<2>;  // + LDS-DMA gather
-    case 32: return &LaunchM1<3>;  // + distinct store data
-    case 33: return &LaunchChunks<K, L, true, false, 3>;          // register gather, packed
-    case 34: return &LaunchChunks<K, L, true, false, 3, true>;    // + two-round staging
-    case 35: return &LaunchChunks<K, L, true, false, 1>;          // 8-byte register gather
-    // Store cache policies (default 0 = nt sc1; see StoreNt16).
-    case 36: return &LaunchChunks<K, L, true, false, 2, false, 16>;  // plain stores
-    case 37: return &LaunchChunks<K, L, true, false, 2, false, 32>;  // sc1
-    case 38: return &LaunchChunks<K, L, true, false, 2, false, 48>;  // sc0 sc1
-    case 39: return &LaunchChunks<K, L, true, false, 2, false, 64>;  // nt (round-2 first cut)
-    case 40: return &LaunchChunks<K, L, true, false, 2, false, 80>;  // sc0 sc1 nt
-    case 41: return &LaunchChunks<K, L, true, false, 2, false, 96>;  // sc0 nt
-    case 42: return &LaunchChunks<K, L, true, false, 3>;             // register gather
-    case 43: return &LaunchChunks<K, L, true, false, 2, true>;       // two-round
-    case 44: return &LaunchChunks<K, L, true, false, 2, false, 512>; // plain (not nt) loads
-    case 45: return &LaunchChunks<K, L, true, false, 2, false, 0, 1>;  // one-wave workgroups
-    case 46: return &LaunchChunks<K, L, true, false, 2, false, 0, 2>;  // two-wave workgroups
-    case 47: return &LaunchChunks<K, L, true, false, 2, false, 2048>;  // + per-wave timeline
-    case 48: return &LaunchPipelined<K, L, true, false>;  // software-pipelined persistent
-    // How the per-wave cost partial is stored (default: lane 0, default
-    // policy, after the output segments).
-    case 49: return &LaunchChunks<K, L, true, false, 2, false, 4096>;   // partial nt sc1
-    case 50: return &LaunchChunks<K, L, true, false, 2, false, 8192>;   // partial sc1
-    case 51: return &LaunchChunks<K, L, true, false, 2, false, 16384>;  // partial first
-    case 52: return &LaunchChunks<K, L, true, false, 2, false, 65536>;  // XCD-grouped slots
-    case 53: return &LaunchChunks<K, L, true, false, 2, false, 32768>;  // no partial (diag.)
-    case 54: return &LaunchStream<K, L, 4>;  // persistent stream, 4 store register sets
-    case 55: return &LaunchStream<K, L, 2>;  // 2 sets
-    case 56: return &LaunchStream<K, L, 1>;  // 1 set (the register hazard kept: A/B)
-    case 57: return &LaunchStream2<K, L, 2>;  // 2 waves per SIMD, 2 sets, two-round staging
-    case 58: return &LaunchStream2<K, L, 1>;  // 2 waves per SIMD, 1 set
-    case 59: return &LaunchChunks<K, L, true, false, 2, false, 131072>;  // XCD-contiguous chunks
-    case 60: return &LaunchChunks<K, L, true, false, 2, false, 262144>;  // chunk-interleaved XCDs
-    case 61: return &LaunchW3<K, L, 524288>;  // twice the FP64 work, 3 waves/SIMD
-    default: return nullptr;
-  }
-}
-
-int AffineVariant() {
-  const char* e = getenv("CSE_AFFINE_VARIANT");
-  return e ? atoi(e) : 0;
-}
-
-// Layout policy of a group: 0 = table, 1 = affine packed cells (BSM),
-// 2 = affine interleaved rows (CRS).
-enum Policy { kTable = 0, kAffinePacked = 1, kAffineCrs = 2 };
 
 // Affine kernels: cooperative slot-0 gather by LDS-DMA from the repacked
 // table (dma = true) or by 8-byte pieces straight from the state.
@@ -367,81 +229,73 @@ LaunchFn PickAffine(bool jac, bool dma) {
 
 template <class K, int L>
 LaunchFn PickJP(bool jac, int policy, bool dma) {
-  switch (policy) {
-    case kAffinePacked: return PickAffine<K, L, false>(jac, dma);
-    case kAffineCrs: return PickAffine<K, L, true>(jac, dma);
-    default: return jac ? &LaunchGeneral<K, L, true> : &LaunchGeneral<K, L, false>;
+  if constexpr (cse::KindTraits<K>::NB <= 2 && cse::KindTraits<K>::NR <= 3) {
+    switch (policy) {
+      case kAffinePacked: return PickAffine<K, L, false>(jac, dma);
+      case kAffineCrs: return PickAffine<K, L, true>(jac, dma);
+      default: break;
+    }
   }
+  return jac ? &LaunchTable<K, L, true> : &LaunchTable<K, L, false>;
 }
 
-template <class K>
-LaunchFn PickL(int loss, bool jac, int policy, bool dma) {
-  switch (loss) {
-    case CSE_LOSS_HUBER: return PickJP<K, cse::kLossHuber>(jac, policy, dma);
-    case CSE_LOSS_CAUCHY: return PickJP<K, cse::kLossCauchy>(jac, policy, dma);
-    default: return PickJP<K, cse::kLossTrivial>(jac, policy, dma);
-  }
+#ifdef CSE_TUNING
+// Tuning build only: alternative settings of the hot kernel (Snavely, BSM,
+// Jacobian, LDS-DMA gather), selected by $CSE_TUNE_VARIANT.
+template <class K, int L, bool J, bool Crs, int Co, class T, int W>
+void LaunchBounded(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksBounded<K, L, J, Crs, Co, T, W>),
+                     dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
 }
 
-LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
-  const int v = AffineVariant();
-  if (v > 0 && kind == CSE_FUNCTOR_SNAVELY_2_9_3 && jac && policy == kAffinePacked) {
-    LaunchFn f = loss == CSE_LOSS_HUBER ? SnavelyVariant<cse::kLossHuber>(v)
-               : loss == CSE_LOSS_TRIVIAL ? SnavelyVariant<cse::kLossTrivial>(v) : nullptr;
-    if (f) return f;
-  }
-  if (!jac && policy != kTable && ValuesVariant() >= 2 && ValuesVariant() <= 4 &&
-      kind == CSE_FUNCTOR_SNAVELY_2_9_3) {
-    // Tuning variants of the Jet-free kernel's camera gather: 2 = 8-byte
-    // pieces from the state, 3 = 16-byte register pieces from the repacked
-    // table (needs dma), 4 = per-lane loads.
-    using SK = cse::SnavelyKind;
-    const int v = ValuesVariant();
-    if (v == 3 && !dma) return nullptr;
-    const bool crs = policy == kAffineCrs;
-#define CSE_VV(L)                                                                    \
-  (v == 2 ? (crs ? &LaunchChunks<SK, L, false, true, 1> : &LaunchChunks<SK, L, false, false, 1>) \
-   : v == 3 ? (crs ? &LaunchChunks<SK, L, false, true, 3> : &LaunchChunks<SK, L, false, false, 3>) \
-            : (crs ? &LaunchChunks<SK, L, false, true, 0> : &LaunchChunks<SK, L, false, false, 0>))
-    return loss == CSE_LOSS_HUBER ? CSE_VV(cse::kLossHuber)
-         : loss == CSE_LOSS_CAUCHY ? CSE_VV(cse::kLossCauchy) : CSE_VV(cse::kLossTrivial);
-#undef CSE_VV
-  }
-  if (!jac && dma && policy != kTable && ValuesVariant() == 1) {
-    // The residual layout is the same for both affine policies.
-    using SK = cse::SnavelyKind;  // the kernel's LDS image is Snavely-shaped
-    if (kind == CSE_FUNCTOR_SNAVELY_2_9_3)
-      return loss == CSE_LOSS_HUBER    ? &LaunchValuesPipelined<SK, cse::kLossHuber>
-           : loss == CSE_LOSS_CAUCHY ? &LaunchValuesPipelined<SK, cse::kLossCauchy>
-                                     : &LaunchValuesPipelined<SK, cse::kLossTrivial>;
-  }
-  switch (kind) {
-    case CSE_FUNCTOR_SNAVELY_2_9_3: return PickL<cse::SnavelyKind>(loss, jac, policy, dma);
-    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3:
-      return PickL<cse::SnavelyNoDistortionKind>(loss, jac, policy, dma);
-    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3:
-      return PickL<cse::SnavelyQuaternionKind>(loss, jac, policy, dma);
-    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3:
-      return PickL<cse::PointDisplacementKind>(loss, jac, policy, dma);
+template <int L>
+LaunchFn TuningVariant(int v) {
+  using K = cse::SnavelyKind;
+  switch (v) {
+    case 1: return &LaunchChunks<K, L, true, false, 2, cse::Tune<1, true>>;
+    case 2: return &LaunchChunks<K, L, true, false, 2, cse::Tune<2, true>>;
+    case 3: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, false>>;
+    case 4: return &LaunchChunks<K, L, true, false, 2, cse::Tune<1, false>>;
+    case 5: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, false>, 4>;
+    case 6: return &LaunchBounded<K, L, true, false, 2, cse::Tune<1, false>, 4>;
+    case 7: return &LaunchBounded<K, L, true, false, 2, cse::Tune<2, false>, 4>;
     default: return nullptr;
   }
 }
 
-// Workgroups per CU of the persistent kernel: LDS-bound (4 waves per
-// workgroup, 64 lanes x staged doubles each) unless overridden by
-// $CSE_WG_PER_CU for tuning.
-int PersistentWgPerCu(const KindShape& k, int policy) {
-  if (const char* e = getenv("CSE_WG_PER_CU")) {
-    const int v = atoi(e);
-    if (v > 0) return v;
-    if (v == 0) return 1 << 20;  // one chunk per wave: not persistent
+LaunchFn TuningPick(int kind, int loss, bool jac, int policy, bool dma) {
+  // Read at every launch, so that one process can A/B the variants.
+  const char* e = getenv("CSE_TUNE_VARIANT");
+  const int v = e ? atoi(e) : 0;
+  if (v <= 0 || kind != CSE_FUNCTOR_SNAVELY_2_9_3 || !jac || policy != kAffinePacked || !dma)
+    return nullptr;
+  switch (loss) {
+    case CSE_LOSS_HUBER: return TuningVariant<cse::kLossHuber>(v);
+    case CSE_LOSS_TRIVIAL: return TuningVariant<cse::kLossTrivial>(v);
+    default: return nullptr;
   }
-  const int v = AffineVariant();
-  if (v == 0 || (v >= 8 && v != 15)) return 1 << 20;  // the non-persistent variants
-  const int lane_doubles = policy == kAffineCrs ? k.nr * (k.s0 + k.s1)
-                                                : k.nr * std::max(k.s0, k.s1);
-  const int lds = cse::kWavesPerBlock * cse::kWave * lane_doubles * 8 + 64;
-  return std::max(1, std::min(8, (160 * 1024) / lds));
+}
+#endif
+
+LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
+#ifdef CSE_TUNING
+  if (LaunchFn f = TuningPick(kind, loss, jac, policy, dma)) return f;
+#endif
+  LaunchFn fn = nullptr;
+  VisitKind(kind, [&](auto kd) {
+    using K = decltype(kd);
+    if constexpr (cse::TestOnly<K>::value) {
+      if (loss == CSE_LOSS_TRIVIAL)
+        fn = jac ? &LaunchTable<K, cse::kLossTrivial, true> : &LaunchTable<K, cse::kLossTrivial, false>;
+    } else {
+      switch (loss) {
+        case CSE_LOSS_HUBER: fn = PickJP<K, cse::kLossHuber>(jac, policy, dma); break;
+        case CSE_LOSS_CAUCHY: fn = PickJP<K, cse::kLossCauchy>(jac, policy, dma); break;
+        default: fn = PickJP<K, cse::kLossTrivial>(jac, policy, dma); break;
+      }
+    }
+  });
+  return fn;
 }
 
 }  // namespace
@@ -471,9 +325,6 @@ struct cse_evaluator {
   std::vector<cse::PlusRun> plus_runs_host;
   DevBuf<cse::PlusRun> plus_runs;
   DevBuf<double> h_delta, h_plus;
-  // Diagnostics: per-wave timestamps of the last evaluation ($CSE_TIMELINE
-  // = output file, written by cse_wait; with CSE_AFFINE_VARIANT=47).
-  DevBuf<uint64_t> timeline;
   DevBuf<int> status;  // [0] running flag, [1] last status
   // Host-path buffers (allocated on first use).
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
@@ -619,6 +470,8 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
                   Group* G) {
   const int64_t n = g.num_blocks;
   if (n == 0) return kTable;
+  // The affine kernels take one or two slots, at most three residuals.
+  if (k.nb > 2 || k.nr > 3 || IsTestKind(g.functor_kind)) return kTable;
   auto gidx = [&](int64_t i) {
     return g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
   };
@@ -724,7 +577,6 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.gradient = grad;
   a.partials = ev->partials.p + G.partial_offset;
   a.status = ev->status.p;
-  a.timeline = ev->timeline.p;
   a.loss.a = G.loss.a;
   a.loss.scale = G.loss.scale;
   a.loss.scaled = G.loss.scaled;
@@ -968,6 +820,8 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown functor kind " + std::to_string(g.functor_kind)));
     if (g.loss.kind < CSE_LOSS_TRIVIAL || g.loss.kind > CSE_LOSS_CAUCHY)
       return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown loss kind " + std::to_string(g.loss.kind)));
+    if (IsTestKind(g.functor_kind) && (g.loss.kind != CSE_LOSS_TRIVIAL || g.loss.scaled))
+      return bail(Fail(CSE_ERR_UNSUPPORTED, "test functor kinds take the trivial loss only"));
     if (g.num_blocks < 0 || (g.num_blocks > 0 && (!g.parameter_block_ids || !g.functor_data)))
       return bail(Fail(CSE_ERR_INVALID, "group " + std::to_string(gi) + " arrays missing"));
     G.kind = g.functor_kind;
@@ -986,7 +840,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
         const int32_t id = g.parameter_block_ids[i * k.nb + j];
         if (id < 0 || id >= d->num_parameter_blocks)
           return bail(Fail(CSE_ERR_INVALID, "parameter block id out of range in group " + std::to_string(gi)));
-        const int want = j == 0 ? k.s0 : k.s1;
+        const int want = k.sz[j];
         const cse_parameter_block& pb = d->parameter_blocks[id];
         if (pb.size != want)
           return bail(Fail(CSE_ERR_INVALID, "parameter block size does not match the functor"));
@@ -1028,25 +882,20 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     if (!G.affine) ev->any_general = true;
     if (G.affine) {
       const int64_t chunks = (g.num_blocks + cse::kWave - 1) / cse::kWave;
-      const int64_t cap = (int64_t)ev->num_cus * PersistentWgPerCu(k, G.policy);
-      G.num_wg = std::max<int64_t>(1, std::min<int64_t>((chunks + cse::kWavesPerBlock - 1) /
-                                                            cse::kWavesPerBlock, cap));
+      G.num_wg = std::max<int64_t>(1, (chunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock);
     } else {
       G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
     }
     // Every kernel writes one cost partial per wave.
-    // Slots are reserved for a multiple of 8 workgroups (the XCD-grouped
-    // slot order, cse::PartialSlot); unused slots stay zero.
     G.partial_offset = ev->total_wg;
-    ev->total_wg += (G.num_wg + 7) / 8 * 8 * cse::kWavesPerBlock;
+    ev->total_wg += G.num_wg * cse::kWavesPerBlock;
     // The LDS-DMA gather reads slot 0 from a repacked copy refreshed every
     // evaluation; worth it while the slot-0 id range is small (BAL: the
     // cameras), otherwise gather 8-byte pieces from the state directly.
     if (G.affine && G.slot0_count > 0 && G.slot0_count <= (1 << 20) &&
-        getenv("CSE_NO_DMA_GATHER") == nullptr &&
         (rc = G.packed0.alloc((size_t)G.slot0_count * G.slot0_stride)))
       return bail(rc);
-    if (G.affine && ev->has_layout && getenv("CSE_ATOMIC_GRADIENT") == nullptr) {
+    if (G.affine && ev->has_layout) {
       const int sizes[2] = {k.s0, k.s1};
       for (int j = 0; j < k.nb; ++j)
         if (GradSupported(k.nr, sizes[j]) && (rc = BuildGradPlan(g, k, j, &G.grad[j], s)))
@@ -1102,11 +951,6 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   if (hipMemsetAsync(ev->partials.p, 0, ev->partials.n * sizeof(double), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "hipMemsetAsync failed"));
   if ((rc = ev->partials2.alloc(kPartialBlocks))) return bail(rc);
-  if (getenv("CSE_TIMELINE")) {
-    int64_t waves = 0;
-    for (auto& G : ev->groups) waves = std::max<int64_t>(waves, G.num_wg * cse::kWavesPerBlock);
-    if ((rc = ev->timeline.alloc(std::max<int64_t>(1, waves) * 8))) return bail(rc);
-  }
   if ((rc = ev->status.alloc(2))) return bail(rc);
   if (hipMemsetAsync(ev->status.p, 0, 2 * sizeof(int), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "memset failed"));
@@ -1133,14 +977,6 @@ int cse_wait(cse_evaluator* ev) {
   if (ev->opts.profile) {
     int rc = FoldTiming(ev);
     if (rc) return rc;
-  }
-  if (ev->timeline.p) {
-    std::vector<uint64_t> h(ev->timeline.n);
-    CSE_HIP(hipMemcpy(h.data(), ev->timeline.p, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    if (FILE* f = fopen(getenv("CSE_TIMELINE"), "wb")) {
-      fwrite(h.data(), sizeof(uint64_t), h.size(), f);
-      fclose(f);
-    }
   }
   return *ev->status_host ? CSE_EVALUATION_FAILED : CSE_OK;
 }
@@ -1196,10 +1032,14 @@ template <class K>
 void LaunchMultiply(const cse::GroupArgs& a, bool affine, bool left, const double* x, double* y,
                     hipStream_t s) {
   const dim3 grid((unsigned)((a.n + cse::kBlockThreads - 1) / cse::kBlockThreads));
-  if (affine && !left)
-    hipLaunchKernelGGL(cse::RightMultiplyAffineKernel<K>, grid, dim3(cse::kBlockThreads), 0, s, a,
-                       x, y);
-  else if (left)
+  if constexpr (cse::KindTraits<K>::NB <= 2) {
+    if (affine && !left) {
+      hipLaunchKernelGGL(cse::RightMultiplyAffineKernel<K>, grid, dim3(cse::kBlockThreads), 0, s,
+                         a, x, y);
+      return;
+    }
+  }
+  if (left)
     hipLaunchKernelGGL((cse::MultiplyTableKernel<K, true>), grid, dim3(cse::kBlockThreads), 0, s,
                        a, x, y);
   else
@@ -1209,18 +1049,7 @@ void LaunchMultiply(const cse::GroupArgs& a, bool affine, bool left, const doubl
 
 bool DispatchMultiply(int kind, const cse::GroupArgs& a, bool affine, bool left, const double* x,
                       double* y, hipStream_t s) {
-  switch (kind) {
-    case CSE_FUNCTOR_SNAVELY_2_9_3:
-      return LaunchMultiply<cse::SnavelyKind>(a, affine, left, x, y, s), true;
-    case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3:
-      return LaunchMultiply<cse::SnavelyNoDistortionKind>(a, affine, left, x, y, s), true;
-    case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3:
-      return LaunchMultiply<cse::SnavelyQuaternionKind>(a, affine, left, x, y, s), true;
-    case CSE_FUNCTOR_POINT_DISPLACEMENT_3_3:
-      return LaunchMultiply<cse::PointDisplacementKind>(a, affine, left, x, y, s), true;
-    default:
-      return false;
-  }
+  return VisitKind(kind, [&](auto kd) { LaunchMultiply<decltype(kd)>(a, affine, left, x, y, s); });
 }
 
 int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double* y, bool left) {
@@ -1372,30 +1201,6 @@ void cse_destroy(cse_evaluator* ev) {
   if (!ev) return;
   (void)hipSetDevice(ev->device);
   if (ev->stream) (void)hipStreamSynchronize(ev->stream);
-  for (auto& G : ev->groups) {
-    G.packed0.release();
-    G.ids.release();
-    G.data.release();
-    G.gindex.release();
-  }
-  ev->pbs.release();
-  ev->cstate.release();
-  ev->plus_jac.release();
-  ev->res_layout.release();
-  ev->jac_layout.release();
-  ev->jac_offsets.release();
-  ev->partials.release();
-  ev->partials2.release();
-  ev->plus_runs.release();
-  ev->timeline.release();
-  ev->h_delta.release();
-  ev->h_plus.release();
-  ev->status.release();
-  ev->h_state.release();
-  ev->h_cost.release();
-  ev->h_res.release();
-  ev->h_jac.release();
-  ev->h_grad.release();
   if (ev->status_host) (void)hipHostFree(ev->status_host);
   for (auto& pr : ev->pending) ev->pool.push_back(pr);
   for (auto& pr : ev->pool) {
@@ -1403,7 +1208,7 @@ void cse_destroy(cse_evaluator* ev) {
     (void)hipEventDestroy(pr.second);
   }
   if (ev->own_stream && ev->stream) (void)hipStreamDestroy(ev->stream);
-  delete ev;
+  delete ev;  // every DevBuf (groups, plans, tables, scratch) frees itself
 }
 
 int cse_get_info(cse_evaluator* ev, cse_info* info) {

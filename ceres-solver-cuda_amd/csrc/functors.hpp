@@ -12,6 +12,16 @@
 
 namespace cse {
 
+// Every kind also offers EvaluateFlat(data, x, r) over its parameter blocks
+// concatenated in slot order (x = [block 0 | block 1 | ...]); the general
+// (table) kernel calls that form, which covers kinds with any number of
+// parameter blocks.  Two-slot kinds forward to their Evaluate.
+#define CSE_FLAT_FROM_TWO_SLOTS                                              \
+  template <typename T>                                                      \
+  static CSE_HD bool EvaluateFlat(const double* d, const T* x, T* r) {       \
+    return Evaluate(d, x, x + kSize0, r);                                    \
+  }
+
 // y = R(angle_axis) x  (include/ceres/rotation.h:830-899): Rodrigues away
 // from theta == 0, the first-order form R = I + hat(w) exactly at zero so
 // Jets still carry the right derivatives.
@@ -79,6 +89,7 @@ struct SnavelyKind {
   static constexpr int kNumResiduals = 2;
   static constexpr int kNumBlocks = 2;
   static constexpr int kSize0 = 9, kSize1 = 3;
+  static constexpr int kSizes[2] = {9, 3};
   static constexpr int kDataSize = 2;
   template <typename T>
   static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
@@ -90,6 +101,7 @@ struct SnavelyKind {
     Project<true>(p, camera[6], camera + 7, obs, r);
     return true;
   }
+  CSE_FLAT_FROM_TWO_SLOTS
 };
 
 // SnavelyReprojectionErrorNoRadialDistortion<2, 7, 3>
@@ -98,6 +110,7 @@ struct SnavelyNoDistortionKind {
   static constexpr int kNumResiduals = 2;
   static constexpr int kNumBlocks = 2;
   static constexpr int kSize0 = 7, kSize1 = 3;
+  static constexpr int kSizes[2] = {7, 3};
   static constexpr int kDataSize = 2;
   template <typename T>
   static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
@@ -109,6 +122,7 @@ struct SnavelyNoDistortionKind {
     Project<false>(p, camera[6], camera, obs, r);
     return true;
   }
+  CSE_FLAT_FROM_TWO_SLOTS
 };
 
 // SnavelyReprojectionErrorWithQuaternions<2, 10, 3>: camera =
@@ -117,6 +131,7 @@ struct SnavelyQuaternionKind {
   static constexpr int kNumResiduals = 2;
   static constexpr int kNumBlocks = 2;
   static constexpr int kSize0 = 10, kSize1 = 3;
+  static constexpr int kSizes[2] = {10, 3};
   static constexpr int kDataSize = 2;
   template <typename T>
   static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
@@ -128,6 +143,7 @@ struct SnavelyQuaternionKind {
     Project<true>(p, camera[7], camera + 8, obs, r);
     return true;
   }
+  CSE_FLAT_FROM_TWO_SLOTS
 };
 
 // PointDisplacementError<3, 3> (internal/ceres/evaluator_cuda_test.cu.cc:84-110).
@@ -135,12 +151,105 @@ struct PointDisplacementKind {
   static constexpr int kNumResiduals = 3;
   static constexpr int kNumBlocks = 1;
   static constexpr int kSize0 = 3, kSize1 = 0;
+  static constexpr int kSizes[1] = {3};
   static constexpr int kDataSize = 3;
   template <typename T>
   static CSE_HD bool Evaluate(const double* xyz, const T* point, const T*, T* r) {
     r[0] = fabs(xyz[0]) - jabs(point[0]);
     r[1] = fabs(xyz[1]) - jabs(point[1]);
     r[2] = fabs(xyz[2]) - jabs(point[2]);
+    return true;
+  }
+  template <typename T>
+  static CSE_HD bool EvaluateFlat(const double* xyz, const T* x, T* r) {
+    return Evaluate(xyz, x, x, r);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Functors of the reference's own known-answer tests.  They are built into
+// the library so that those tests run through the product kernels (the
+// general/table path; cse_functor_kind values 100+).  Not used by BAL.
+// ---------------------------------------------------------------------------
+
+// ParameterIgnoringCostFunction<kFactor, kR, Ns...>
+// (internal/ceres/evaluator_test.cc:58-100) written as the linear functor
+//   r_i = (i + 1) + kFactor * sum_b sum_j (j + 1) x_b[j]:
+// at the zero state the reference's test evaluates at, its value i + 1 and
+// its Jacobian columns kFactor * (j + 1) are exactly what the fake returns.
+// data = {kFactor, succeeds}; succeeds == 0 makes the functor return false
+// (EvaluatorAbortsForResidualsThatFailToEvaluate, :535-553).
+template <int kR, int... Ns>
+struct LinearTestKind {
+  static constexpr int kNumResiduals = kR;
+  static constexpr int kNumBlocks = sizeof...(Ns);
+  static constexpr bool kTestOnly = true;
+  static constexpr int kSizes[kNumBlocks] = {Ns...};
+  static constexpr int kSize0 = kSizes[0], kSize1 = kNumBlocks > 1 ? kSizes[1] : 0;
+  static constexpr int kDataSize = 2;
+  template <typename T>
+  static CSE_HD bool EvaluateFlat(const double* d, const T* x, T* r) {
+    T acc(0.0);
+    int q = 0;
+#pragma unroll
+    for (int b = 0; b < kNumBlocks; ++b)
+#pragma unroll
+      for (int j = 0; j < kSizes[b]; ++j, ++q) acc = acc + (double)(j + 1) * x[q];
+#pragma unroll
+    for (int i = 0; i < kR; ++i) r[i] = (double)(i + 1) + d[0] * acc;
+    return d[1] != 0.0;
+  }
+};
+
+// BinaryScalarCost (internal/ceres/autodiff_cost_function_cuda_test.cu.cc:40-51):
+// cost = x0 y0 + x1 y1 - a, parameter blocks x[2], y[2]; data = {a}.
+struct BilinearTestKind {
+  static constexpr bool kTestOnly = true;
+  static constexpr int kNumResiduals = 1;
+  static constexpr int kNumBlocks = 2;
+  static constexpr int kSizes[2] = {2, 2};
+  static constexpr int kSize0 = 2, kSize1 = 2;
+  static constexpr int kDataSize = 1;
+  template <typename T>
+  static CSE_HD bool EvaluateFlat(const double* d, const T* x, T* r) {
+    r[0] = x[0] * x[2] + x[1] * x[3] - d[0];
+    return true;
+  }
+};
+
+// TenParameterCost (autodiff_cost_function_cuda_test.cu.cc:123-139): ten
+// parameter blocks of size one, cost = x0 + ... + x9.  The functor has no
+// constants; its one data double is unused.
+struct TenParameterTestKind {
+  static constexpr bool kTestOnly = true;
+  static constexpr int kNumResiduals = 1;
+  static constexpr int kNumBlocks = 10;
+  static constexpr int kSizes[10] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+  static constexpr int kSize0 = 1, kSize1 = 1;
+  static constexpr int kDataSize = 1;
+  template <typename T>
+  static CSE_HD bool EvaluateFlat(const double*, const T* x, T* r) {
+    r[0] = x[0] + x[1] + x[2] + x[3] + x[4] + x[5] + x[6] + x[7] + x[8] + x[9];
+    return true;
+  }
+};
+
+// OnlyFillsOneOutputFunctor (autodiff_cost_function_cuda_test.cu.cc:224-230):
+// two residuals, only the first assigned.  AutoDifferentiate pre-fills the
+// outputs with kImpossibleValue (include/ceres/internal/autodiff.h:355-360)
+// and ResidualBlock::Evaluate rejects them (residual_block.cc:146-152,
+// array_utils.cc:44-53), so the evaluation fails.
+struct PartialOutputTestKind {
+  static constexpr bool kTestOnly = true;
+  static constexpr int kNumResiduals = 2;
+  static constexpr int kNumBlocks = 1;
+  static constexpr int kSizes[1] = {1};
+  static constexpr int kSize0 = 1, kSize1 = 0;
+  static constexpr int kDataSize = 1;
+  static constexpr bool kMayLeaveOutputs = true;
+  template <typename T>
+  static CSE_HD bool EvaluateFlat(const double*, const T* x, T* r) {
+    r[0] = x[0];
     return true;
   }
 };

@@ -36,6 +36,14 @@ struct Jet {
 #pragma unroll
     for (int i = 0; i < N; ++i) v[i] = 0.0;
   }
+  // Value and every partial set to x (AutoDifferentiate's kImpossibleValue
+  // pre-fill of the outputs, autodiff.h:355-360).
+  static CSE_HD Jet Filled(double x) {
+    Jet r; r.a = x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = x;
+    return r;
+  }
   // The k-th infinitesimal seeded (autodiff.h:185-199).
   CSE_HD Jet(double value, int k) : a(value) {
 #pragma unroll

@@ -1,0 +1,346 @@
+// kernel_common.hpp -- shared pieces of the gfx950 evaluator kernels.
+//
+// Kernel arguments, compile-time functor shapes, the autodiff of one
+// residual block (include/ceres/internal/autodiff.h:314-381), the loss and
+// Corrector step (cuda_evaluator_kernel.h:373-407 / residual_block.cc:
+// 159-199), LDS-staged wave stores and the inline-asm store primitives.
+#ifndef CSE_KERNEL_COMMON_HPP_
+#define CSE_KERNEL_COMMON_HPP_
+
+#include <stdint.h>
+
+#include "functors.hpp"
+#include "jet.hpp"
+#include "loss.hpp"
+
+namespace cse {
+
+constexpr int kBlockThreads = 256;
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = kBlockThreads / kWave;
+constexpr int kMaxSlots = 10;  // parameter blocks per residual block (table path)
+
+// kImpossibleValue (internal/ceres/array_utils.h:52): the marker
+// AutoDifferentiate pre-fills outputs with.
+constexpr double kImpossibleValue = 1e302;
+
+// Device copy of a parameter block (table path).
+struct PbDev {
+  int64_t state_offset;
+  int64_t delta_offset;
+  int64_t plus_jacobian_offset;
+  int32_t tangent_size;
+  int32_t is_constant;
+};
+
+struct GroupArgs {
+  int64_t n;
+  const int32_t* ids;   // [n][kNumBlocks]
+  const double* data;   // [n][kDataSize]
+  const double* state;
+  const double* cstate;
+  const PbDev* pbs;
+  const double* plus_jacobians;
+  // Affine policy.
+  int64_t state_base[2];
+  int64_t delta_base[2];
+  int64_t res_base;
+  int64_t jac_base[2][3];
+  int64_t jac_stride[2];
+  // Slot-0 parameter blocks repacked at a 16-byte-aligned stride (the
+  // affine path's cooperative LDS-DMA gather; see RepackSlot0Kernel).
+  const double* packed0;
+  int32_t packed0_lo;
+  int32_t packed0_stride;  // doubles per block, even
+  // Table policy.
+  const int64_t* gindex;
+  int64_t first;
+  const int64_t* residual_layout;
+  const int64_t* jac_layout;
+  const int64_t* jac_offsets;
+  // Outputs.
+  double* residuals;
+  double* jacobian;
+  double* gradient;
+  double* partials;
+  int* status;
+  // Fused gradient (EvaluateAffineChunksFused, see FusedGrad): the gradient
+  // (delta offsets), the slot-1 wave-boundary entries [2 * chunks][4] and
+  // the slot-0 per-block contributions J0^T r [n][S0p].
+  double* gfused;
+  double* gside;
+  double* gcontrib;
+  LossParams loss;
+  int apply_loss;
+  int check_finite;
+};
+
+// Compile-time shape of a functor kind: kR residuals, NB parameter blocks
+// of sizes kSizes[0..NB) concatenated into N columns.
+template <class K>
+constexpr int SlotOffset(int j) {
+  int o = 0;
+  for (int b = 0; b < j; ++b) o += K::kSizes[b];
+  return o;
+}
+template <class K>
+constexpr int MaxSlotSize() {
+  int m = 0;
+  for (int b = 0; b < K::kNumBlocks; ++b) m = K::kSizes[b] > m ? K::kSizes[b] : m;
+  return m;
+}
+template <class K>
+struct KindTraits {
+  static constexpr int NR = K::kNumResiduals;
+  static constexpr int NB = K::kNumBlocks;
+  static constexpr int S0 = K::kSize0;
+  static constexpr int S1 = NB > 1 ? K::kSize1 : 0;
+  static constexpr int S1p = S1 > 0 ? S1 : 1;
+  static constexpr int D = K::kDataSize;
+  static constexpr int N = SlotOffset<K>(NB);
+  static constexpr int Size(int j) { return K::kSizes[j]; }
+  static constexpr int Off(int j) { return SlotOffset<K>(j); }
+  static constexpr int MaxSize() { return MaxSlotSize<K>(); }
+};
+
+// Does the kind declare that it may leave outputs unassigned?
+template <class K, class = void>
+struct MayLeaveOutputs {
+  static constexpr bool value = false;
+};
+template <class K>
+struct MayLeaveOutputs<K, decltype((void)K::kMayLeaveOutputs)> {
+  static constexpr bool value = K::kMayLeaveOutputs;
+};
+
+// Is the kind one of the known-answer-test functors (general path, trivial
+// loss only)?
+template <class K, class = void>
+struct TestOnly {
+  static constexpr bool value = false;
+};
+template <class K>
+struct TestOnly<K, decltype((void)K::kTestOnly)> {
+  static constexpr bool value = K::kTestOnly;
+};
+
+// Any of x[0..n) NaN or infinite?  An integer test on the exponent field:
+// the TU is compiled with -ffinite-math-only, which would fold isfinite().
+template <int kCount>
+CSE_HD bool AnyNonFinite(const double* x) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < kCount; ++i) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x[i]);
+    m = max(m, (uint32_t)(b >> 32) & 0x7ff00000u);
+  }
+  return m == 0x7ff00000u;
+}
+
+// Any of x[0..n) equal to kImpossibleValue (an unassigned output)?  Bit
+// comparison, for the same reason.
+template <int kCount>
+CSE_HD bool AnyImpossible(const double* x) {
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < kCount; ++i)
+    any = any || __builtin_bit_cast(uint64_t, x[i]) == __builtin_bit_cast(uint64_t, kImpossibleValue);
+  return any;
+}
+
+// Deterministic workgroup sum: xor-butterfly inside each wave, then the
+// waves in a fixed order.  Returns the sum in thread 0.
+__device__ __forceinline__ double WorkgroupSum(double v, double* lds) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) t += lds[w];
+  }
+  return t;
+}
+
+// Copy `count` doubles, staged contiguously in LDS by this wave, to global
+// memory at dst with all 64 lanes: 16-byte stores when dst is 16-byte
+// aligned (1 KiB per wave instruction), 8-byte stores otherwise.
+__device__ __forceinline__ void WaveStore(const double* lds, double* dst, int count, int lane) {
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int pairs = count >> 1;
+    for (int t = lane; t < pairs; t += kWave) {
+      const double2 v = *reinterpret_cast<const double2*>(lds + 2 * t);
+      __builtin_nontemporal_store(v.x, dst + 2 * t);
+      __builtin_nontemporal_store(v.y, dst + 2 * t + 1);
+    }
+    if ((count & 1) && lane == 0) dst[count - 1] = lds[count - 1];
+  } else {
+    for (int t = lane; t < count; t += kWave) dst[t] = lds[t];
+  }
+}
+
+// AutoDifferentiate (include/ceres/internal/autodiff.h:314-381) for the
+// two-slot affine kernels: seed one Jet per parameter with its unit vector,
+// pre-fill the outputs with kImpossibleValue (:355-360), run the functor,
+// split the partials into the row-major per-block Jacobians.  kJac = false
+// runs the functor on plain doubles.
+template <class K, bool kJac>
+CSE_HD bool EvaluateFunctor(const double* d, const double* x0, const double* x1, double* r,
+                            double* J0, double* J1) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = S0 + S1;
+  if constexpr (kJac) {
+    Jet<N> j0[S0], j1[S1p], out[NR];
+#pragma unroll
+    for (int k = 0; k < S0; ++k) j0[k] = Jet<N>(x0[k], k);
+#pragma unroll
+    for (int k = 0; k < S1; ++k) j1[k] = Jet<N>(x1[k], S0 + k);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) out[k] = Jet<N>::Filled(kImpossibleValue);
+    const bool ok = K::Evaluate(d, j0, j1, out);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      r[k] = out[k].a;
+#pragma unroll
+      for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+#pragma unroll
+      for (int c = 0; c < S1; ++c) J1[k * S1p + c] = out[k].v[S0 + c];
+    }
+    return ok;
+  } else {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) r[k] = kImpossibleValue;
+    return K::Evaluate(d, x0, x1, r);
+  }
+}
+
+// The same over the concatenated parameter vector x[N] of any number of
+// slots (the table kernel): J is kR x N row-major, slot j in columns
+// [Off(j), Off(j) + Size(j)).
+template <class K, bool kJac>
+CSE_HD bool EvaluateFunctorFlat(const double* d, const double* x, double* r, double* J) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, N = Tr::N;
+  if constexpr (kJac) {
+    Jet<N> xj[N], out[NR];
+#pragma unroll
+    for (int k = 0; k < N; ++k) xj[k] = Jet<N>(x[k], k);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) out[k] = Jet<N>::Filled(kImpossibleValue);
+    const bool ok = K::EvaluateFlat(d, xj, out);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      r[k] = out[k].a;
+#pragma unroll
+      for (int c = 0; c < N; ++c) J[k * N + c] = out[k].v[c];
+    }
+    return ok;
+  } else {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) r[k] = kImpossibleValue;
+    return K::EvaluateFlat(d, x, r);
+  }
+}
+
+// Loss and correction (cuda_evaluator_kernel.h:373-407 /
+// residual_block.cc:159-199) on r and the per-slot Jacobians J0 (kR x S0)
+// and J1 (kR x S1).  Returns the block cost.
+template <class K, int kLoss, bool kJac>
+CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, double* J0,
+                             double* J1) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  double sq = 0.0;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) sq += r[k] * r[k];
+  const bool robust = (kLoss != kLossTrivial || lp.scaled) && apply_loss;
+  if (!robust) return 0.5 * sq;
+  double rho[3];
+  EvaluateLoss<kLoss>(lp, sq, rho);
+  const Corrector corr(sq, rho);
+  if constexpr (kJac) {
+    corr.template CorrectJacobian<NR, S0>(r, J0);
+    if constexpr (S1 > 0) corr.template CorrectJacobian<NR, S1p>(r, J1);
+  }
+  corr.template CorrectResiduals<NR>(r);
+  return 0.5 * rho[0];
+}
+
+// ---------------------------------------------------------------------------
+// Inline-asm store primitives.  Why the affine kernel's stores are inline
+// asm (measured, tools/membench2.hip): on gfx950 a vector-memory store
+// reads its address and data VGPRs after issue, when the store reaches the
+// head of the CU's memory queue.  An instruction that overwrites one of
+// those VGPRs before then stalls the wave until the store drains -- under a
+// saturated write stream that is microseconds -- so a wave whose register
+// allocator reuses a store's VGPRs for the next store's address issues its
+// stores one queue-drain at a time (1.64 ms against 1.24 ms for the same
+// memory path with the stores back to back).  These stores take operands
+// the compiler keeps live to the end of the kernel (KeepAlive).
+// ---------------------------------------------------------------------------
+typedef int cse_v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ cse_v4i AsV4i(double a, double b) {
+  const double2 v = make_double2(a, b);
+  cse_v4i d;
+  __builtin_memcpy(&d, &v, 16);
+  return d;
+}
+
+// 16-byte store at base + kOff bytes (kOff in [-4096, 4095]).  kPol: the
+// cache policy, 0 = nt sc1 (streaming, not kept in the XCD's L2; 6-8 %
+// faster than nt alone on the evaluator's output stream, profiles/r02),
+// 1 = default policy, 2 = nt.
+template <int kOff, int kPol = 0>
+__device__ __forceinline__ void StoreNt16(double* base, const cse_v4i& d) {
+  static_assert(kOff >= -4096 && kOff <= 4095, "global offset out of range");
+  if constexpr (kPol == 1)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2" ::"v"(base), "v"(d), "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 2)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 nt" ::"v"(base), "v"(d), "i"(kOff)
+                 : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1 nt" ::"v"(base), "v"(d),
+                 "i"(kOff)
+                 : "memory");
+}
+
+// Pieces kJ.. of a wave segment: piece j of lane l at b + 16 * (64 (j % 8))
+// - 4096 bytes, b = b0 for j < 8 and b1 after (1 KiB per instruction).
+template <int kJ, int kCount, int kPol = 0>
+__device__ __forceinline__ void SegmentStoresFrom(double* b0, double* b1, const cse_v4i* q) {
+  if constexpr (kJ < kCount) {
+    StoreNt16<(kJ % 8) * 1024 - 4096, kPol>(kJ < 8 ? b0 : b1, q[kJ]);
+    SegmentStoresFrom<kJ + 1, kCount, kPol>(b0, b1, q);
+  }
+}
+
+// One double (8-byte vector store, default cache policy) from the calling
+// lanes; the caller masks.  Both operands are VGPRs computed before the
+// store tail.
+__device__ __forceinline__ void StoreB64(double* addr, double value) {
+  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(addr), "v"(value) : "memory");
+}
+__device__ __forceinline__ void StoreB32(int* addr, int value) {
+  asm volatile("global_store_dword %0, %1, off" ::"v"(addr), "v"(value) : "memory");
+}
+// One double at addr + kOff bytes, default cache policy (the fused
+// gradient's scattered slot-1 rows: neighbouring lanes share lines in L2).
+template <int kOff>
+__device__ __forceinline__ void StoreB64At(double* addr, double value) {
+  asm volatile("global_store_dwordx2 %0, %1, off offset:%2" ::"v"(addr), "v"(value), "i"(kOff)
+               : "memory");
+}
+
+template <int kCount>
+__device__ __forceinline__ void KeepAlive(const cse_v4i* q) {
+#pragma unroll
+  for (int j = 0; j < kCount; ++j) asm volatile("" ::"v"(q[j]));
+}
+
+}  // namespace cse
+
+#endif  // CSE_KERNEL_COMMON_HPP_

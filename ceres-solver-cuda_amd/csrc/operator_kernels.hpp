@@ -1,0 +1,572 @@
+// operator_kernels.hpp -- the kernels around the evaluation: the gradient
+// post-pass and the fused gradient's tails, the Jacobian as a linear
+// operator (J x, J^T x, the CGNR normal operator), Program::Plus, the cost
+// reduction and the slot-0 repack.
+#ifndef CSE_OPERATOR_KERNELS_HPP_
+#define CSE_OPERATOR_KERNELS_HPP_
+
+#include "evaluate_kernel.hpp"
+
+namespace cse {
+
+// ---------------------------------------------------------------------------
+// Gradient g = J^T r as a deterministic post-pass over the outputs just
+// written (affine groups with residuals and Jacobian requested).  The
+// reference adds J^T r with per-element FP64 atomics inside the evaluate
+// kernel (cuda_evaluator_kernel.h:149-160); with ~2,100 observations per
+// camera and 64 random addresses per wave instruction those atomics ran at
+// 18 ms per evaluation here (0.05 of the HBM roofline).  Instead, for each
+// slot, the blocks are listed per parameter block (counting sort at create
+// time; identity for the points of a Schur-ordered problem) and every
+// parameter block sums its blocks' J_b^T r_b in a fixed order:
+//   kWaveMode = false: one lane per parameter block (few blocks each:
+//                      points), true: one wave per parameter block (many
+//                      blocks each: cameras), lanes strided over the blocks
+//                      and a fixed xor-butterfly.
+// ---------------------------------------------------------------------------
+struct GradArgs {
+  const double* jac;
+  int64_t jrow[3];   // start of row k of the slot's cell for block 0
+  int64_t jstride;   // per block
+  const double* res;
+  int64_t res_base;
+  const int32_t* perm;  // blocks sorted by parameter block; null = identity
+  const int64_t* off;   // [count + 1]
+  int64_t count;        // parameter blocks lo .. lo + count - 1
+  int32_t lo;
+  double* grad;
+  int64_t delta_base;   // delta offset of id = delta_base + S * id
+};
+
+template <int NR, int S, bool kWaveMode>
+__global__ __launch_bounds__(kBlockThreads) void GradientSlotKernel(const GradArgs g) {
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  int64_t p;
+  int64_t q0, q1, qs;
+  if constexpr (kWaveMode) {
+    p = ((int64_t)blockIdx.x * kBlockThreads + threadIdx.x) / kWave;
+    if (p >= g.count) return;
+    q0 = g.off[p] + (threadIdx.x & (kWave - 1));
+    q1 = g.off[p + 1];
+    qs = kWave;
+  } else {
+    p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+    if (p >= g.count) return;
+    q0 = g.off[p];
+    q1 = g.off[p + 1];
+    qs = 1;
+  }
+  for (int64_t q = q0; q < q1; q += qs) {
+    const int64_t b = g.perm ? (int64_t)g.perm[q] : q;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double rk = g.res[g.res_base + (int64_t)NR * b + k];
+      const double* row = g.jac + g.jrow[k] + g.jstride * b;
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[c] += row[c] * rk;
+    }
+  }
+  double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+  if constexpr (kWaveMode) {
+#pragma unroll
+    for (int c = 0; c < S; ++c)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) dst[c] += acc[c];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < S; ++c) dst[c] += acc[c];
+  }
+}
+
+// Parameter blocks with many blocks (cameras): their block lists are cut
+// into chunks of at most kGradChunk blocks, one wave per chunk
+// (GradientLanesKernel), and GradientChunkReduceKernel adds each parameter
+// block's chunk partials in order.  Deterministic, no atomics.  (An
+// element-per-lane variant that reads whole cells per instruction measured
+// 3-10 % slower: the random cells and residual pairs cost whole lines
+// either way.)
+constexpr int kGradChunk = 512;
+
+struct GradChunks {
+  const int64_t* begin;      // [nchunks + 1] chunk c covers perm[begin[c], begin[c+1])
+  const int64_t* chunk_off;  // [count + 1] chunks of parameter block p
+  double* partial;           // [nchunks][S]
+  int64_t nchunks;
+};
+
+// Lane per block: each lane reads its blocks' whole cells
+// (rows of S contiguous doubles) and residual pairs; S accumulators per
+// lane, combined by a fixed xor-butterfly.
+template <int NR, int S>
+__global__ __launch_bounds__(kBlockThreads) void GradientLanesKernel(const GradArgs g,
+                                                                     const GradChunks ch) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (cid >= ch.nchunks) return;
+  const int64_t q1 = ch.begin[cid + 1];
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
+    const int64_t b = g.perm ? (int64_t)g.perm[q] : q;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double rk = g.res[g.res_base + (int64_t)NR * b + k];
+      const double* row = g.jac + g.jrow[k] + g.jstride * b;
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[c] += row[c] * rk;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < S; ++c)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < S; ++c) ch.partial[cid * S + c] = acc[c];
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const GradArgs g,
+                                                                           const GradChunks ch) {
+  const int64_t p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (p >= g.count) return;
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q)
+#pragma unroll
+    for (int c = 0; c < S; ++c) acc[c] += ch.partial[q * S + c];
+  double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+#pragma unroll
+  for (int c = 0; c < S; ++c) dst[c] += acc[c];
+}
+
+// Fused-gradient slot 0 (FusedGrad): each chunk of a parameter block's
+// block list sums the blocks' written contributions (S of the SP doubles
+// per block; two 64-byte sectors per block instead of the Jacobian cell
+// and residual pair), a fixed butterfly, then GradientChunkReduceKernel.
+template <int S, int SP>
+__global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const double* contrib,
+                                                                       const int32_t* perm,
+                                                                       const GradChunks ch) {
+  static_assert(SP % 2 == 0 && SP >= S, "16-byte records");
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (cid >= ch.nchunks) return;
+  const int64_t q1 = ch.begin[cid + 1];
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
+    const double2* rec = reinterpret_cast<const double2*>(contrib + (int64_t)SP * perm[q]);
+#pragma unroll
+    for (int h = 0; h < SP / 2; ++h) {
+      const double2 v = rec[h];
+      if (2 * h < S) acc[2 * h] += v.x;
+      if (2 * h + 1 < S) acc[2 * h + 1] += v.y;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < S; ++c)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < S; ++c) ch.partial[cid * S + c] = acc[c];
+  }
+}
+
+// Fused-gradient slot 1: the waves' boundary entries (sum[S], id) are in
+// wave order, so their ids are non-decreasing; the first entry of each id
+// adds that id's entries in order and adds the sum to the row (no interior
+// run of any wave touched these rows).
+template <int S>
+__global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const double* side,
+                                                                        int64_t count,
+                                                                        double* grad,
+                                                                        int64_t delta_base) {
+  static_assert(S <= 3, "entries hold 3 sums and the id");
+  const int64_t e = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (e >= count) return;
+  const double key = side[4 * e + 3];
+  if (e > 0 && side[4 * (e - 1) + 3] == key) return;
+  double acc[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) acc[c] = 0.0;
+  for (int64_t f = e; f < count && side[4 * f + 3] == key; ++f)
+#pragma unroll
+    for (int c = 0; c < S; ++c) acc[c] += side[4 * f + c];
+  double* dst = grad + delta_base + (int64_t)S * (int64_t)key;
+#pragma unroll
+  for (int c = 0; c < S; ++c) dst[c] += acc[c];
+}
+
+// Identity order (the points of a Schur-ordered problem): one 64-thread
+// workgroup per 64 consecutive parameter blocks, whose blocks form one
+// contiguous range.  The range is walked in tiles of 64 blocks: all lanes
+// form the products J[e] * r[k] element by element (contiguous loads), park
+// them in LDS, and then thread t sums parameter block t's blocks of the
+// tile in block, row order.
+template <int NR, int S>
+__global__ __launch_bounds__(kWave) void GradientRangeKernel(const GradArgs g) {
+  constexpr int E = NR * S;
+  constexpr int T = kWave;  // blocks per tile
+  __shared__ double prod[T * E];
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kWave;
+  const int64_t p = p0 + lane;
+  const int64_t pend = p0 + kWave < g.count ? p0 + kWave : g.count;
+  const int64_t B0 = g.off[p0], B1 = g.off[pend];
+  const int64_t my0 = p < g.count ? g.off[p] : B1, my1 = p < g.count ? g.off[p + 1] : B1;
+  double acc[S];
+#pragma unroll
+  for (int cc = 0; cc < S; ++cc) acc[cc] = 0.0;
+  for (int64_t t0 = B0; t0 < B1; t0 += T) {
+    const int nb = B1 - t0 < T ? (int)(B1 - t0) : T;
+#pragma unroll
+    for (int it = 0; it < E; ++it) {
+      const int t = it * kWave + lane;  // element t of the tile
+      const int bm = t / E, e = t - bm * E, k = e / S, cc = e - k * S;
+      double v = 0.0;
+      if (bm < nb) {
+        const int64_t b = t0 + bm;
+        v = g.jac[g.jrow[k] + g.jstride * b + cc] * g.res[g.res_base + (int64_t)NR * b + k];
+      }
+      prod[t] = v;
+    }
+    __syncthreads();
+    const int64_t lo = my0 > t0 ? my0 : t0, hi = my1 < t0 + nb ? my1 : t0 + nb;
+    for (int64_t b = lo; b < hi; ++b) {
+      const int bm = (int)(b - t0);
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+#pragma unroll
+        for (int cc = 0; cc < S; ++cc) acc[cc] += prod[bm * E + k * S + cc];
+    }
+    __syncthreads();
+  }
+  if (p < g.count) {
+    double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+#pragma unroll
+    for (int cc = 0; cc < S; ++cc) dst[cc] += acc[cc];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The Jacobian as a linear operator (cse_jacobian_right/left_multiply):
+// y += J x and y += J^T x on the values this evaluator wrote.  The affine
+// J^T x reuses the gradient post-pass kernels (x in place of r).
+// ---------------------------------------------------------------------------
+template <class K>
+__global__ __launch_bounds__(kBlockThreads) void RightMultiplyAffineKernel(const GroupArgs a,
+                                                                           const double* x,
+                                                                           double* y) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1;
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (i >= a.n) return;
+  const int2 id = LoadIds<K>(a, i);
+  const double* x0 = x + a.delta_base[0] + (int64_t)S0 * id.x;
+  double acc[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const double* row = a.jacobian + a.jac_base[0][k] + a.jac_stride[0] * i;
+    double t = 0.0;
+#pragma unroll
+    for (int c = 0; c < S0; ++c) t += row[c] * x0[c];
+    acc[k] = t;
+  }
+  if constexpr (NB == 2) {
+    const double* x1 = x + a.delta_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double* row = a.jacobian + a.jac_base[1][k] + a.jac_stride[1] * i;
+#pragma unroll
+      for (int c = 0; c < S1; ++c) acc[k] += row[c] * x1[c];
+    }
+  }
+  double* yb = y + a.res_base + (int64_t)NR * i;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) yb[k] += acc[k];
+}
+
+// Table path (any layout, constant blocks, tangent sizes): the reference's
+// WriteJacobians addressing (cuda_evaluator_kernel.h:260-294).
+template <class K, bool kLeft>
+__global__ __launch_bounds__(kBlockThreads) void MultiplyTableKernel(const GroupArgs a,
+                                                                     const double* x, double* y) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB;
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (i >= a.n) return;
+  const int64_t gi = a.gindex ? a.gindex[i] : a.first + i;
+  const int64_t res = a.residual_layout[gi];
+  int64_t q = a.jac_layout[gi];
+  double acc[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) acc[k] = 0.0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const PbDev pb = a.pbs[a.ids[i * NB + j]];
+    if (pb.is_constant) continue;
+    const int S = Tr::Size(j);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double* row = a.jacobian + a.jac_offsets[q++];
+      for (int c = 0; c < S; ++c) {
+        if (c >= pb.tangent_size) break;
+        if constexpr (kLeft)
+          unsafeAtomicAdd(y + pb.delta_offset + c, row[c] * x[res + k]);
+        else
+          acc[k] += row[c] * x[pb.delta_offset + c];
+      }
+    }
+  }
+  if constexpr (!kLeft) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) y[res + k] += acc[k];
+  }
+}
+
+// The CGNR normal operator in one pass over J (cse_cgnr_multiply):
+// y += J^T (J x), replacing CudaCgnrLinearOperator::RightMultiplyAndAccumulate
+// (internal/ceres/cgnr_solver.cc:226-237), which runs z = J x and y += J^T z
+// as two sparse products (two reads of J and a round trip of z).  One wave
+// per 64-block chunk, as the evaluator:
+//   * the wave's Jacobian image (BSM: its F then E segments; CRS: its rows)
+//     comes in by LDS-DMA, 1 KiB per instruction, and each lane reads its
+//     block's cells from LDS;
+//   * z_b = J_b x (two values) stays in registers;
+//   * slot 1 (points): E_b^T z_b through the fused gradient's segmented
+//     scan -- interior runs add into y directly, the wave's first and last
+//     runs go to boundary entries (GradientBoundaryKernel adds them);
+//   * slot 0 (cameras): F_b^T z_b in block order (GradientContribKernel and
+//     GradientChunkReduceKernel add them per camera, fixed order).
+// Deterministic; the host requires the fused gradient's eligibility.
+template <class K, bool kCrs>
+__global__ __launch_bounds__(kBlockThreads) void CgnrMultiplyKernel(const GroupArgs a,
+                                                                    const double* x, double* y) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, N = Tr::N;
+  static_assert(Tr::NB == 2 && NR == 2 && S1 == 3, "Snavely-shaped groups");
+  constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kImg = kWave * NR * N;        // doubles of one wave's Jacobian image
+  constexpr int kPieces = kImg / (2 * kWave);  // 16-byte DMA pieces per lane
+  static_assert(kImg % (2 * kWave) == 0 && (kWave * NR * S0) % (2 * kWave) == 0, "16-B pieces");
+  __shared__ double img[kWavesPerBlock][kImg];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t nchunks = (a.n + kWave - 1) / kWave;
+  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (c >= nchunks) return;
+  double* im = img[wave];
+  const int64_t i0 = c * kWave;
+  const int nw = a.n - i0 < kWave ? (int)(a.n - i0) : kWave;
+  const bool active = lane < nw;
+  const int64_t i = active ? i0 + lane : a.n - 1;
+  const long long idw = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
+  const int id0 = (int)idw, id1 = (int)(idw >> 32);
+
+  // Column c of row k of slot j for this lane's block, at LDS offset
+  // off[j][k] + c (full chunks) -- or straight from HBM (the last chunk).
+  const int64_t row0 = kCrs ? (a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0]
+                                                                     : a.jac_base[1][0])
+                            : 0;
+  double F[NR * S0], E[NR * S1];
+  if (nw == kWave) {
+    if constexpr (kCrs) {
+      const double* seg = a.jacobian + row0 + (int64_t)NR * N * i0;
+#pragma unroll
+      for (int k = 0; k < kPieces; ++k)
+        __builtin_amdgcn_global_load_lds(seg + 2 * (k * kWave + lane), im + 2 * kWave * k, 16, 0, 0);
+    } else {
+      const double* segF = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+      const double* segE = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
+      constexpr int kF = kWave * NR * S0 / (2 * kWave);
+#pragma unroll
+      for (int k = 0; k < kF; ++k)
+        __builtin_amdgcn_global_load_lds(segF + 2 * (k * kWave + lane), im + 2 * kWave * k, 16, 0, 0);
+#pragma unroll
+      for (int k = 0; k < kPieces - kF; ++k)
+        __builtin_amdgcn_global_load_lds(segE + 2 * (k * kWave + lane), im + 2 * kWave * (kF + k),
+                                         16, 0, 0);
+    }
+  }
+  double xc[S0], xp[S1];
+  {
+    const double* x0 = x + a.delta_base[0] + (int64_t)S0 * id0;
+    const double* x1 = x + a.delta_base[1] + (int64_t)S1 * id1;
+#pragma unroll
+    for (int k = 0; k < S0; ++k) xc[k] = x0[k];
+#pragma unroll
+    for (int k = 0; k < S1; ++k) xp[k] = x1[k];
+  }
+  if (nw == kWave) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int f0 = kCrs ? (int)(a.jac_base[0][k] - row0) + NR * N * lane : NR * S0 * lane + S0 * k;
+      const int e0 = kCrs ? (int)(a.jac_base[1][k] - row0) + NR * N * lane
+                          : kWave * NR * S0 + NR * S1 * lane + S1 * k;
+#pragma unroll
+      for (int cc = 0; cc < S0; ++cc) F[k * S0 + cc] = im[f0 + cc];
+#pragma unroll
+      for (int cc = 0; cc < S1; ++cc) E[k * S1 + cc] = im[e0 + cc];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const double* rf = a.jacobian + a.jac_base[0][k] + a.jac_stride[0] * i;
+      const double* re = a.jacobian + a.jac_base[1][k] + a.jac_stride[1] * i;
+#pragma unroll
+      for (int cc = 0; cc < S0; ++cc) F[k * S0 + cc] = rf[cc];
+#pragma unroll
+      for (int cc = 0; cc < S1; ++cc) E[k * S1 + cc] = re[cc];
+    }
+  }
+  double z[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    double t = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < S0; ++cc) t += F[k * S0 + cc] * xc[cc];
+#pragma unroll
+    for (int cc = 0; cc < S1; ++cc) t += E[k * S1 + cc] * xp[cc];
+    z[k] = active ? t : 0.0;
+  }
+  // J_b^T z_b: FusedGrad with z in place of r (its J1 rows are S1p = S1 wide).
+  FusedGrad<K> fg;
+  fg.Compute(z, F, E, id1, active, lane, nw, c);
+  if (fg.interior) {
+    double* row = y + a.delta_base[1] + (int64_t)S1 * fg.key;
+    row[0] += fg.g1[0];
+    row[1] += fg.g1[1];
+    row[2] += fg.g1[2];
+  }
+  if (fg.writer) {
+    double4* e = reinterpret_cast<double4*>(a.gside + 4 * fg.entry);
+    *e = make_double4(fg.g1[0], fg.g1[1], fg.g1[2], fg.g1[3]);
+  }
+  if (nw == 1 && lane == 0)
+    *reinterpret_cast<double4*>(a.gside + 4 * (2 * c + 1)) = make_double4(0.0, 0.0, 0.0, fg.g1[3]);
+  if (nw == kWave) {
+    // Camera contributions: staged (the image has been read), 16-B pieces.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < S0p / 2; ++j)
+      reinterpret_cast<double2*>(im)[lane * (S0p / 2) + j] = make_double2(fg.g0[2 * j], fg.g0[2 * j + 1]);
+    __builtin_amdgcn_wave_barrier();
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    v2d* dst = reinterpret_cast<v2d*>(a.gcontrib + (int64_t)S0p * i0);
+#pragma unroll
+    for (int j = 0; j < S0p / 2; ++j)
+      __builtin_nontemporal_store(reinterpret_cast<const v2d*>(im)[j * kWave + lane],
+                                  dst + j * kWave + lane);
+  } else if (active) {
+    double* dst = a.gcontrib + (int64_t)S0p * i;
+#pragma unroll
+    for (int cc = 0; cc < S0p; ++cc) dst[cc] = fg.g0[cc];
+  }
+}
+
+// y += D .* D .* x (CudaVector::DtDxpy, cgnr_solver.cc:236).
+__global__ __launch_bounds__(kBlockThreads) void DtDxpyKernel(const double* D, const double* x,
+                                                              double* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (i < n) y[i] += D[i] * D[i] * x[i];
+}
+
+// Program::Plus for manifold-free blocks: runs of consecutive state entries
+// whose delta offset is a constant shift away (one run for a BAL problem).
+struct PlusRun {
+  int64_t state_begin;
+  int64_t length;
+  int64_t delta_shift;  // delta index = state index - delta_shift
+};
+
+__global__ __launch_bounds__(kBlockThreads) void PlusKernel(const double* x, const double* delta,
+                                                            double* out, const PlusRun* runs,
+                                                            int num_runs) {
+  for (int r = 0; r < num_runs; ++r) {
+    const PlusRun run = runs[r];
+    for (int64_t t = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x; t < run.length;
+         t += (int64_t)gridDim.x * kBlockThreads) {
+      const int64_t i = run.state_begin + t;
+      out[i] = x[i] + delta[i - run.delta_shift];
+    }
+  }
+}
+
+// First pass of the cost reduction when there are many partials: workgroup
+// b sums partials [b*per, (b+1)*per) in a fixed order.
+__global__ __launch_bounds__(kBlockThreads) void PartialSumKernel(const double* partials,
+                                                                  int64_t n, int64_t per,
+                                                                  double* out) {
+  __shared__ double lds_sum[kWavesPerBlock];
+  const int64_t begin = (int64_t)blockIdx.x * per;
+  const int64_t end = begin + per < n ? begin + per : n;
+  double v = 0.0;
+  for (int64_t k = begin + threadIdx.x; k < end; k += kBlockThreads) v += partials[k];
+  const double t = WorkgroupSum(v, lds_sum);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
+}
+
+// Sums the per-workgroup partials of every group in a fixed order, writes
+// the cost, publishes the evaluation status and re-arms the status word
+// for the next evaluation (replaces thrust::reduce + the abort-flag round
+// trip, autodiff_residual_block_cuda_evaluator.h:241-265).
+__global__ __launch_bounds__(1024) void FinalizeKernel(const double* partials, int64_t n,
+                                                       double* cost, int* status,
+                                                       int* status_out) {
+  __shared__ double wsum[1024 / kWave];
+  // Four independent accumulators per thread keep several loads in flight.
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+  const int64_t step = blockDim.x;
+  int64_t k = threadIdx.x;
+  for (; k + 3 * step < n; k += 4 * step) {
+    v0 += partials[k];
+    v1 += partials[k + step];
+    v2 += partials[k + 2 * step];
+    v3 += partials[k + 3 * step];
+  }
+  for (; k < n; k += step) v0 += partials[k];
+  double v = (v0 + v1) + (v2 + v3);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) t += wsum[w];
+    const int s = *status;
+    *cost = s ? 0.0 : t;
+    *status_out = s;
+    *status = 0;
+  }
+}
+
+// Copies slot-0 parameter blocks [lo, lo + count) of the state into the
+// packed table at a 16-byte-aligned stride (once per evaluation: 13,682
+// cameras = 1.1 MB for BAL problem-13682).
+__global__ __launch_bounds__(256) void RepackSlot0Kernel(const double* state, int64_t state_base,
+                                                         int size, int stride, int32_t lo,
+                                                         int64_t count, double* packed) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = t / stride;
+  const int k = (int)(t - b * stride);
+  if (b >= count) return;
+  packed[t] = k < size ? state[state_base + (int64_t)size * (lo + b) + k] : 0.0;
+}
+
+}  // namespace cse
+
+#endif  // CSE_OPERATOR_KERNELS_HPP_

@@ -54,7 +54,27 @@ typedef enum cse_functor_kind {
   CSE_FUNCTOR_SNAVELY_2_9_3 = 0,
   CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3 = 1,
   CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 = 2,
-  CSE_FUNCTOR_POINT_DISPLACEMENT_3_3 = 3
+  CSE_FUNCTOR_POINT_DISPLACEMENT_3_3 = 3,
+  /* The functors of the reference's own known-answer tests, so that those
+   * tests run through the library's kernels (general path, trivial loss
+   * only).  kind                      kR  blocks      data
+   *   TEST_LINEAR_<kR>_<sizes>           see name    kFactor, succeeds
+   *       ParameterIgnoringCostFunction, internal/ceres/evaluator_test.cc:58-100,
+   *       as r_i = (i+1) + kFactor sum_b sum_j (j+1) x_b[j] (exact at x = 0)
+   *   TEST_BILINEAR_1_2_2             1   2,2         a
+   *       BinaryScalarCost, autodiff_cost_function_cuda_test.cu.cc:40-51
+   *   TEST_TEN_PARAMETER_1_x10        1   1 (x10)     unused
+   *       TenParameterCost, autodiff_cost_function_cuda_test.cu.cc:123-139
+   *   TEST_PARTIAL_OUTPUT_2_1         2   1           unused
+   *       OnlyFillsOneOutputFunctor, autodiff_cost_function_cuda_test.cu.cc:224-230 */
+  CSE_FUNCTOR_TEST_LINEAR_3_2_3_4 = 100,
+  CSE_FUNCTOR_TEST_LINEAR_3_4_3_2 = 101,
+  CSE_FUNCTOR_TEST_LINEAR_2_2_3 = 102,
+  CSE_FUNCTOR_TEST_LINEAR_3_2_4 = 103,
+  CSE_FUNCTOR_TEST_LINEAR_4_3_4 = 104,
+  CSE_FUNCTOR_TEST_BILINEAR_1_2_2 = 110,
+  CSE_FUNCTOR_TEST_TEN_PARAMETER_1_x10 = 111,
+  CSE_FUNCTOR_TEST_PARTIAL_OUTPUT_2_1 = 112
 } cse_functor_kind;
 
 /* LossFunctionCUDA variants, include/ceres/loss_function_cuda.h:62-150. */

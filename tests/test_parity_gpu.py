@@ -195,6 +195,63 @@ def test_division_by_zero_depth_fails(gpu):
     assert ref[0] is False and got[0] is False
 
 
+def _two_slot_problem(kind, loss, n=200, seed=5):
+    """A small problem of one two-slot kind (Snavely-shaped) with a mix of
+    small and large residuals, so that Huber's inlier and outlier branches
+    both run."""
+    rng = np.random.default_rng(seed)
+    s0 = ca.FUNCTOR_SHAPES[kind][1][0]
+    p = ca.ProblemCUDA()
+    cams = []
+    for c in range(4):
+        if kind == ca.SNAVELY_QUATERNION_2_10_3:
+            q = rng.normal(size=4)
+            cam = np.concatenate([q / np.linalg.norm(q), [0.1, -0.2, -10.0], [800.0, 0.01, 0.001]])
+        else:
+            cam = np.concatenate([rng.normal(0, 0.05, 3), [0.1, -0.2, -10.0], [800.0, 0.01, 0.001]])
+        cams.append(p.add_parameter_block(cam[:s0]))
+    pts = [p.add_parameter_block(rng.uniform(-3, 3, 3)) for _ in range(n // 4)]
+    for i in range(n):
+        obs = rng.normal(0, 300.0, 2)
+        p.add_residual_block(kind, loss, obs, cams[i % 4], pts[i // 4])
+    prog = p.program()
+    prog.compile(ca.BLOCK_SPARSE, num_eliminate_blocks=0)
+    return prog
+
+
+@pytest.mark.parametrize("kind", [ca.SNAVELY_2_9_3, ca.SNAVELY_NO_DISTORTION_2_7_3,
+                                  ca.SNAVELY_QUATERNION_2_10_3, ca.POINT_DISPLACEMENT_3_3])
+@pytest.mark.parametrize("loss", [None, ca.Loss.huber(1.0), ca.Loss.huber(1e6), ca.Loss.cauchy(1.0)])
+@pytest.mark.parametrize("where", ["param-nan", "param-inf", "data-nan", "data-inf"])
+def test_non_finite_inputs_fail_every_functor_and_loss(gpu, kind, loss, where):
+    # The kernels are built with -ffinite-math-only; the evaluation must still
+    # reject NaN/Inf outputs (residual_block.cc:146-152) on every functor and
+    # every loss branch (Huber a = 1: outliers; a = 1e6: inliers), on both
+    # the affine and the table path, as the CPU ProgramEvaluator does.
+    if kind == ca.POINT_DISPLACEMENT_3_3:
+        p = ca.ProblemCUDA()
+        rng = np.random.default_rng(9)
+        blocks = [p.add_parameter_block(rng.normal(size=3)) for _ in range(70)]
+        for b in blocks:
+            p.add_residual_block(kind, loss, rng.normal(size=3), b)
+        prog = p.program()
+        prog.compile(ca.BLOCK_SPARSE)
+    else:
+        prog = _two_slot_problem(kind, loss)
+    bad = np.nan if where.endswith("nan") else np.inf
+    if where.startswith("param"):
+        prog.state[len(prog.state) // 2] = bad
+    else:
+        prog.groups[0].data[prog.groups[0].n // 3, 0] = bad
+    ref = oracle_eval(prog, threads=1)
+    assert ref[0] is False
+    for general in (False, True):
+        got, _ = gpu_eval(prog, force_general_layout=general)
+        assert got[0] is False, (general, where)
+        got, _ = gpu_eval(prog, force_general_layout=general, gradient=False, jacobian=False)
+        assert got[0] is False, (general, where, "residuals only")
+
+
 @pytest.mark.parametrize("n_obs", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
 def test_ragged_sizes(gpu, n_obs):
     n_pts = max(1, n_obs // 3)

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""A/B timing of the hot kernel's tuning variants (tuning build only).
+
+Loads lib/libcse_tuning.so (make -C ceres-solver-cuda_amd tuning), builds one
+problem-13682-shaped Program, and times the residual+Jacobian evaluation for
+each $CSE_TUNE_VARIANT in interleaved rounds (so box drift hits all variants
+alike).  Every variant's residuals, Jacobian and cost are checked bit-equal
+to variant 0's (the variants change how the outputs are written, not what).
+
+  python tools/ab_bench.py --variants 0,1,2,3,5 --rounds 3 --steps 20
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
+
+import numpy as np  # noqa: E402
+
+from ceres_amd import _cse  # noqa: E402
+
+_cse.use_library(os.path.join(REPO, "ceres-solver-cuda_amd", "lib", "libcse_tuning.so"))
+
+import ceres_amd as ca  # noqa: E402
+from ceres_amd import bal  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--config", default="problem-13682-4456117")
+    ap.add_argument("--loss", default="huber")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    import torch
+    variants = [int(v) for v in args.variants.split(",")]
+    loss = {"huber": ca.Loss.huber(1.0), "trivial": ca.Loss.trivial()}[args.loss]
+    t0 = time.time()
+    prog = bal.synthetic_program(args.config, loss=loss)
+    print(f"# built {args.config} in {time.time() - t0:.1f} s", flush=True)
+    dev = torch.device("cuda", 0)
+    f64 = torch.float64
+    state = torch.from_numpy(prog.state).to(dev)
+    cost = torch.zeros(1, dtype=f64, device=dev)
+    res = torch.empty(prog.num_residuals, dtype=f64, device=dev)
+    jac = torch.empty(prog.num_jacobian_values, dtype=f64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ref_hash = None
+    times = {v: [] for v in variants}
+    bytes_ = None
+    for rnd in range(args.rounds):
+        for v in variants:
+            os.environ["CSE_TUNE_VARIANT"] = str(v)
+            ev = ca.Evaluator(prog, device=0, profile=True, stream=stream.cuda_stream)
+            bytes_ = ev.info().bytes_jacobian_eval
+            for _ in range(3):
+                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None,
+                                   jac.data_ptr())
+            assert ev.wait() == 0
+            if rnd == 0:
+                h = hashlib.sha1()
+                h.update(res.cpu().numpy().tobytes())
+                h.update(jac[:: 97].cpu().numpy().tobytes())
+                h.update(jac[-100000:].cpu().numpy().tobytes())
+                h.update(cost.cpu().numpy().tobytes())
+                digest = h.hexdigest()
+                if ref_hash is None:
+                    ref_hash = digest
+                same = digest == ref_hash
+                print(f"# variant {v}: outputs {'identical' if same else 'DIFFER'}", flush=True)
+            ev.reset_kernel_stats()
+            for _ in range(args.steps):
+                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None,
+                                   jac.data_ptr())
+            assert ev.wait() == 0
+            _, total, n = ev.kernel_stats()
+            ev.close()
+            ms = total / n
+            times[v].append(ms)
+            print(f"round {rnd} variant {v}: {ms:.4f} ms  {bytes_ / ms / 1e6:.0f} GB/s  "
+                  f"frac {bytes_ / ms / 1e6 / 8000:.3f}", flush=True)
+    summary = {v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                   "frac_median": bytes_ / float(np.median(t)) / 1e6 / 8000} for v, t in times.items()}
+    print(json.dumps(summary))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"config": args.config, "loss": args.loss, "times_ms": times,
+                       "summary": summary}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
