@@ -8,23 +8,42 @@ eliminated first: BASELINE.json configs[3]) through the C ABI's
 device-resident entry point (cse_evaluate_device: residuals, Jacobian values
 and cost written to HBM; inputs already resident when the clock starts).
 
-Multi-GPU (one process per GPU, launched by torch.distributed.run):
-  --scaling weak   (default) every rank evaluates its own problem-13682-sized
-                   shard (a distinct seed) of an N x larger global problem;
-                   the scalar cost is all-reduced over RCCL each step.
-                   value = N * steps / time.
-  --scaling strong the one problem-13682 is partitioned at point-bucket
-                   boundaries (BASELINE.json configs[4]); each rank writes
-                   its contiguous Jacobian strips; cost all-reduced over RCCL.
-                   value = steps / time.
+Multi-GPU (BASELINE.json configs[4]), one process per GPU:
+  `bench.py --gpus N` starts the N ranks itself (torch.distributed.run in a
+  child process, before anything touches a GPU) unless it already runs under
+  a launcher (WORLD_SIZE set, which must equal N).
+  --scaling strong (default) the one problem-13682 is cut into N point-bucket
+                   shards (ceres_amd.shard / ceres_amd.distributed); each rank
+                   evaluates its shard and writes its contiguous Jacobian
+                   strips; the cost (and, with the gradient, the camera rows)
+                   is all-reduced over RCCL.  value = whole-problem
+                   evaluations / s.
+  --scaling weak   every rank evaluates its own problem-13682-sized replica
+                   (a distinct seed); value = N * steps / time.
+  With more ranks than visible GPUs (a rehearsal on a 1-GPU box) the ranks
+  share the devices and the exchange runs over gloo; the line says so.
 
-Data is synthetic (no BAL file is available offline; see
-ceres_amd/bal.py for the generator), with the exact BAL header counts.
-Rank 0 prints one JSON line; see DESIGN.md §5 for every field.
+Besides the headline, the default line carries secondary legs measured in the
+same run (each with its own barrier-bracketed timing, max over ranks):
+  gradient       residual+Jacobian+gradient J^T r (what the trust-region
+                 minimizer requests, trust_region_minimizer.cc:242-255)
+  residual_only  residuals + cost (trust_region_minimizer.cc:770-788)
+  host_strips    evaluation + D2H of each rank's residual and Jacobian
+                 strips into pinned host memory (the reference's seam,
+                 README.md:198-200; PCIe-inclusive, never `value`)
+and, on rank 0 at N=1, the CPU baseline (the oracle, oracle/, built
+-O3 -march=native on this host) at 1 thread and at the box's CPU share, for
+residual+Jacobian and residual-only.
+
+Data is synthetic (no BAL file is available offline; see ceres_amd/bal.py for
+the generator), with the exact BAL header counts.  Rank 0 prints one JSON
+line; DESIGN.md §5 documents every field.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,7 +53,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
 
 import ceres_amd as ca  # noqa: E402
-from ceres_amd import bal, shard  # noqa: E402
+from ceres_amd import bal  # noqa: E402
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "residual+Jacobian evaluations/sec on BAL problem-13682; achieved HBM GB/s"
@@ -48,8 +67,9 @@ def parse():
     ap.add_argument("--config", default="problem-13682-4456117", choices=list(bal.CONFIGS))
     ap.add_argument("--loss", default="huber", choices=["trivial", "huber", "cauchy"])
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--gradient", action="store_true", help="also produce the gradient J^T r")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--gradient", action="store_true",
+                    help="the headline step also produces the gradient J^T r")
     ap.add_argument("--gradient-mode", type=int, default=0, choices=[0, 1, 2],
                     help="cse_options.gradient_mode: 0 fused (default), 1 post-pass, 2 atomics")
     ap.add_argument("--mode", default="jacobian",
@@ -58,17 +78,34 @@ def parse():
                          "residual: residuals+cost only; candidate: the trust-region candidate "
                          "step, Plus(x, delta) then cost-only evaluation "
                          "(trust_region_minimizer.cc:770-788); spmv: one CGNR iteration's "
-                         "products J p and J^T (J p) on the evaluated Jacobian (cgnr_solver.cc)")
+                         "products J p and J^T (J p); cgnr: the one-pass normal operator")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the gradient / residual-only / host-strip legs")
+    ap.add_argument("--secondary-steps", type=int, default=20)
+    ap.add_argument("--host-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-blocks", type=int, default=0,
-                    help="0 = the whole workload (about 1 s per eval on 16 cores)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the box's CPU share ($OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
-    ap.add_argument("--host-copy", action="store_true",
-                    help="also time evaluations that copy the rank's residuals and Jacobian "
-                         "strips to pinned host memory (the reference's D2H seam; reported "
-                         "under 'host_copy', never as value)")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """Start args.gpus ranks of this script under torch.distributed.run, as a
+    child process (this process has not touched a GPU), and return its exit
+    code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def make_loss(name):
@@ -76,226 +113,293 @@ def make_loss(name):
             "cauchy": ca.Loss.cauchy(1.0)}[name]
 
 
-def build_shard(args, rank, world):
-    counts = bal.CONFIGS[args.config]
-    loss = make_loss(args.loss)
-    if args.scaling == "weak" or world == 1:
-        cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed + rank)
-        prog = bal.program(cams, pts, ci, pi, obs, loss=loss, format=args.format)
-        return prog, {"blocks": int(counts[2]), "strip": None}
-    cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed)
-    prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss,
-                                   format=args.format)
-    strips = [[g, g + n] for _, g, n in sh.jacobian_strips()]
-    return prog, {"blocks": sh.blocks[1] - sh.blocks[0], "strip": strips}
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle restatement of ProgramEvaluator
+# ---------------------------------------------------------------------------
+def _host_info():
+    model, phys = None, set()
+    pid = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    phys.add((pid, v))
+    except OSError:
+        pass
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(),
+            "sockets": len({p for p, _ in phys}) or None, "physical_cores": len(phys) or None,
+            "affinity_cpus": len(os.sched_getaffinity(0))}
 
 
-def cpu_baseline(args, threads):
-    """The oracle (CPU restatement of Ceres' ProgramEvaluator, oracle/) on a
-    bounded, point-bucket-aligned sample of the same workload."""
+def _oracle_module():
+    """oracle_py bound to a -O3 -march=native build made on this host (into
+    /tmp), else the portable prebuilt one."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py as O
-    counts = bal.CONFIGS[args.config]
-    cams, pts, ci, pi, obs = bal.synthetic(*counts, seed=args.seed)
-    S = min(args.cpu_sample_blocks or counts[2], counts[2])
-    # Cut at a point-bucket boundary.
-    last_pt = int(pi[S - 1])
-    S = int(np.searchsorted(pi, last_pt, side="right"))
-    np_ = last_pt + 1
-    prog = bal.program(cams, pts[:np_], ci[:S], pi[:S], obs[:S], loss=make_loss(args.loss),
-                       format=args.format)
-    op = O.OracleProgram.from_program(prog)
-    ev = op.evaluator(threads)
-    r = np.empty(prog.num_residuals)
-    j = np.empty(prog.num_jacobian_values)
-    g = np.empty(prog.num_effective_parameters) if args.gradient else None
-    ev.run(prog.state, None, r, g, j)  # warm-up
-    times = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        ok, _ = ev.run(prog.state, None, r, g, j)
-        times.append(time.perf_counter() - t0)
-        assert ok
-    ev.close()
-    t = float(np.median(times))
-    blocks_per_s = S / t
-    return {"value": blocks_per_s / counts[2], "unit": "evals/s", "cores": threads,
-            "kind": "port",
-            "sample": (f"all {S:,} residual blocks" if S == counts[2] else
-                   f"first {S:,} of {counts[2]:,} residual blocks (point-bucket aligned)") +
-                  f" of the same workload, residual+Jacobian{'+gradient' if args.gradient else ''}, "
-                  f"median of 3 evals = {t * 1e3:.1f} ms; value = blocks/s / {counts[2]:,}",
-            "blocks_per_sec": blocks_per_s}
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"cse_oracle_native_{os.getpid()}")
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "native",
+                        f"NATIVE_OUT={out}"], check=True, capture_output=True, timeout=120)
+        O.use_library(os.path.join(out, "liboracle_native.so"))
+        build = "g++ -O3 -march=native (oracle/Makefile native, built on this host)"
+    except Exception as e:  # noqa: BLE001 - a missing compiler leaves the portable build
+        build = f"portable prebuilt build (-O3, no -march=native; native build failed: {e!r})"
+    return O, build
 
 
+def cpu_baseline(args, arrays, threads):
+    """The oracle on bounded, point-bucket-aligned samples of the workload:
+    residual+Jacobian and residual-only, at `threads` and at 1 thread.
+    value = the multithreaded residual+Jacobian rate, in whole-workload
+    evaluations per second (blocks per second / the workload's blocks)."""
+    O, build = _oracle_module()
+    cams, pts, ci, pi, obs = arrays
+    total = len(ci)
+
+    cache = {}
+
+    def sample(nblocks):
+        if nblocks in cache:
+            return cache[nblocks]
+        S = min(nblocks, total)
+        last_pt = int(pi[S - 1])
+        S = int(np.searchsorted(pi, last_pt, side="right"))
+        prog = bal.program(cams, pts[:last_pt + 1], ci[:S], pi[:S], obs[:S],
+                           loss=make_loss(args.loss), format=args.format)
+        cache[nblocks] = (S, prog)
+        return S, prog
+
+    legs = {}
+    for jac in (True, False):
+        for nt in (threads, 1):
+            # about 1 s per timed evaluation: the whole workload multithreaded,
+            # a 1/16 (Jacobian) or 1/8 (residual-only) sample on one thread
+            S, prog = sample(total if nt > 1 else total // (16 if jac else 8))
+            ev = O.OracleProgram.from_program(prog).evaluator(nt)
+            r = np.empty(prog.num_residuals)
+            j = np.empty(prog.num_jacobian_values) if jac else None
+            ev.run(prog.state, None, r, None, j)  # warm-up (page faults)
+            times = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                ok, _ = ev.run(prog.state, None, r, None, j)
+                times.append(time.perf_counter() - t0)
+                assert ok
+            ev.close()
+            t = float(np.median(times))
+            legs[f"{'jacobian' if jac else 'residual'}_{nt}t"] = {
+                "evals_per_s": S / t / total, "blocks_per_s": S / t, "threads": nt,
+                "sample_blocks": S, "median_s": t}
+            del r, j
+    head = legs[f"jacobian_{threads}t"]
+    return {"value": head["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
+            "sample": (f"residual+Jacobian of all {total:,} residual blocks of the same workload "
+                       f"on {threads} threads, median of 3 after a warm-up; legs: 1-thread runs "
+                       f"on the first 1/16 (Jacobian) or 1/8 (residual-only) of the blocks, cut "
+                       f"at a point bucket; value = blocks/s / {total:,}"),
+            "build": build, "host": _host_info(), "legs": legs}
+
+
+# ---------------------------------------------------------------------------
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    # One process per GPU.  (Ranks beyond the visible devices share them:
-    # that only happens in a 1-GPU rehearsal of the multi-rank path, which
-    # also sets CSE_DIST_BACKEND=gloo since RCCL needs distinct devices.)
-    dev_index = local_rank % max(1, torch.cuda.device_count())
+    from ceres_amd import distributed
+
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py needs a HIP device")
+    rehearsal = world > ndev  # several ranks per device: gloo, not RCCL
+    dev_index = local_rank % ndev
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    backend = os.environ.get("CSE_DIST_BACKEND", "nccl")
+    backend = os.environ.get("CSE_DIST_BACKEND", "gloo" if rehearsal else "nccl")
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
 
-    t_build = time.perf_counter()
-    prog, shard_info = build_shard(args, rank, world)
-    build_s = time.perf_counter() - t_build
+    def reduce_max(vals):
+        if world == 1:
+            return vals
+        on_host = backend == "gloo"
+        t = torch.tensor(vals, dtype=torch.float64, device="cpu" if on_host else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t.cpu()]
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    strong = args.scaling == "strong"
+    t_build = time.perf_counter()
+    counts = bal.CONFIGS[args.config]
+    arrays = bal.synthetic(*counts, seed=args.seed + (0 if strong else rank))
+    srank, sworld = (rank, world) if strong else (0, 1)
     stream = torch.cuda.current_stream(dev)
-    ev = ca.Evaluator(prog, device=dev_index, profile=True, stream=stream.cuda_stream,
-                      gradient_mode=args.gradient_mode)
+    se = distributed.ShardedEvaluator(*arrays, srank, sworld, device=dev_index,
+                                      loss=make_loss(args.loss), format=args.format,
+                                      gradient=True, gradient_mode=args.gradient_mode,
+                                      stream=stream)
+    if not (rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "jacobian"):
+        del arrays
+        arrays = None
+    build_s = time.perf_counter() - t_build
+    ev, prog = se.evaluator, se.program
     info = ev.info()
     f64 = torch.float64
-    state = torch.from_numpy(prog.state).to(dev)
-    cost = torch.zeros(1, dtype=f64, device=dev)
-    res = torch.empty(prog.num_residuals, dtype=f64, device=dev)
-    jac = torch.empty(prog.num_jacobian_values, dtype=f64, device=dev)
-    grad = torch.empty(prog.num_effective_parameters, dtype=f64, device=dev) if args.gradient else None
-    gptr = grad.data_ptr() if grad is not None else None
+    units = world if not strong else 1  # whole-problem evaluations per step
 
+    def run_leg(step, steps, warmup):
+        """Warm-up, then `steps` timed steps between barrier + synchronize;
+        returns (elapsed_s, kernel_ms_local, kernel_ms_max) maxed over ranks."""
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if se.wait() != 0:
+            raise SystemExit(f"rank {rank}: evaluation failed during warm-up")
+        ev.reset_kernel_stats()
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        status = se.wait()
+        _, total_ms, launches = ev.kernel_stats()
+        kernel_ms = total_ms / max(launches, 1)
+        elapsed_max, kernel_max, status_max = reduce_max([elapsed, kernel_ms, float(status)])
+        if status_max != 0:
+            raise SystemExit(f"evaluation failed (status {status_max})")
+        return elapsed_max, kernel_ms, kernel_max
+
+    # ---- the headline step -------------------------------------------------
+    if args.mode in ("spmv", "cgnr"):
+        se.evaluate(residuals=True, jacobian=True, gradient=False)
+        ne = prog.num_effective_parameters
+        pvec = torch.ones(ne, dtype=f64, device=dev)
+        dvec = torch.full((ne,), 0.5, dtype=f64, device=dev)
+        jp = torch.zeros(prog.num_residuals, dtype=f64, device=dev)
+        jtjp = torch.zeros(ne, dtype=f64, device=dev)
     if args.mode == "candidate":
         delta = torch.full((prog.num_effective_parameters,), 1e-6, dtype=f64, device=dev)
-        cand = torch.empty_like(state)
-    if args.mode in ("spmv", "cgnr"):
-        ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None, jac.data_ptr())
-        pvec = torch.ones(prog.num_effective_parameters, dtype=f64, device=dev)
-        dvec = torch.full((prog.num_effective_parameters,), 0.5, dtype=f64, device=dev)
-        jp = torch.zeros(prog.num_residuals, dtype=f64, device=dev)
-        jtjp = torch.zeros(prog.num_effective_parameters, dtype=f64, device=dev)
+        cand = torch.empty_like(se.state)
 
     def step():
         if args.mode == "jacobian":
-            ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), gptr,
-                               jac.data_ptr())
+            se.evaluate(residuals=True, jacobian=True, gradient=args.gradient)
         elif args.mode == "residual":
-            ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None, None)
+            se.evaluate(residuals=True, jacobian=False, gradient=False)
         elif args.mode == "candidate":
-            ev.plus_device(state.data_ptr(), delta.data_ptr(), cand.data_ptr())
-            ev.evaluate_device(cand.data_ptr(), cost.data_ptr(), None, None, None)
+            ev.plus_device(se.state.data_ptr(), delta.data_ptr(), cand.data_ptr())
+            ev.evaluate_device(cand.data_ptr(), se.cost.data_ptr(), None, None, None)
+            if se.exchange:
+                se._all_reduce(se.cost)
         elif args.mode == "cgnr":  # one pass: J^T J p + D^2 p (cse_cgnr_multiply)
-            ev.cgnr_multiply_device(jac.data_ptr(), dvec.data_ptr(), pvec.data_ptr(),
+            ev.cgnr_multiply_device(se.jacobian.data_ptr(), dvec.data_ptr(), pvec.data_ptr(),
                                     jtjp.data_ptr())
-            return
         else:
-            ev.right_multiply_device(jac.data_ptr(), pvec.data_ptr(), jp.data_ptr())
-            ev.left_multiply_device(jac.data_ptr(), jp.data_ptr(), jtjp.data_ptr())
-            return
-        if world > 1:
-            dist.all_reduce(cost)  # RCCL over xGMI: the global cost
+            ev.right_multiply_device(se.jacobian.data_ptr(), pvec.data_ptr(), jp.data_ptr())
+            ev.left_multiply_device(se.jacobian.data_ptr(), jp.data_ptr(), jtjp.data_ptr())
 
-    for _ in range(args.warmup):
-        step()
-    status = ev.wait()
-    if status != 0:
-        raise SystemExit(f"rank {rank}: evaluation failed during warm-up (status {status})")
-    ev.reset_kernel_stats()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    status = ev.wait()
-    last_ms, total_ms, launches = ev.kernel_stats()
-    kernel_ms = total_ms / max(launches, 1)
-    if args.mode in ("spmv", "cgnr"):  # no evaluate launches in the timed loop: the step time
-        kernel_ms = elapsed / args.steps * 1e3
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=f64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms_max = float(t[0]), float(t[1])
-        ok = torch.tensor([status], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MAX)
-        status = int(ok.item())
-    else:
-        kernel_ms_max = kernel_ms
-    if status != 0:
-        raise SystemExit(f"evaluation failed (status {status})")
+    elapsed, kernel_ms, kernel_ms_max = run_leg(step, args.steps, args.warmup)
+    if args.mode in ("spmv", "cgnr"):  # no evaluate launches in the loop: the step time
+        kernel_ms = kernel_ms_max = elapsed / args.steps * 1e3
 
-    host_copy = None
-    if args.host_copy:
-        # The reference's seam: outputs handed back in host memory.  Each rank
-        # copies its contiguous residual and Jacobian strips (shard.Shard) to
-        # pinned buffers on the evaluator's stream.
-        hres = torch.empty(prog.num_residuals, dtype=f64, pin_memory=True)
-        hjac = torch.empty(prog.num_jacobian_values, dtype=f64, pin_memory=True)
+    # Compulsory bytes per launch on this rank (SURVEY.md §8 d).
+    ne, nres, nj = prog.num_effective_parameters, prog.num_residuals, prog.num_jacobian_values
+    bytes_launch = {
+        "jacobian": info.bytes_jacobian_eval + (8 * ne if args.gradient else 0),
+        "residual": info.bytes_residual_eval,
+        # the timed kernel is the cost-only evaluation (no residual stores)
+        "candidate": info.bytes_residual_eval - 8 * nres,
+        "spmv": 2 * 8 * nj,  # J read twice (vectors are small next to it)
+        "cgnr": 8 * nj + 4 * 8 * ne,  # J once, p, D and y
+    }[args.mode]
+    def reduce_sum(v):
+        if world == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=f64, device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(t)
+        return float(t.item())
 
-        def step_host():
-            step()
-            hres.copy_(res, non_blocking=True)
-            hjac.copy_(jac, non_blocking=True)
+    tot_bytes = reduce_sum(bytes_launch)
+    # Per GPU: the ranks' bytes / N over the slowest rank's kernel time.
+    achieved = tot_bytes / world / (kernel_ms_max * 1e-3) / 1e9
+    value = units * args.steps / elapsed
 
-        step_host()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        th = time.perf_counter()
-        for _ in range(args.steps):
-            step_host()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        eh = time.perf_counter() - th
-        if world > 1:
-            t = torch.tensor([eh], dtype=f64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            eh = float(t[0])
-        d2h = (prog.num_residuals + prog.num_jacobian_values) * 8
-        host_copy = {
-            "value": (world if (args.scaling == "weak" or world == 1) else 1) * args.steps / eh,
-            "unit": "evals/s", "ms_per_step": eh / args.steps * 1e3,
-            "d2h_bytes_per_rank": d2h, "d2h_GBps_per_rank": d2h * args.steps / eh / 1e9,
-            "what": "device evaluation + D2H of the rank's residual and Jacobian strips into "
-                    "pinned host memory, every step (PCIe-inclusive; not the headline value)"}
+    # ---- secondary legs --------------------------------------------------
+    secondary = {}
+    if args.mode == "jacobian" and not args.no_secondary:
+        ks = args.secondary_steps
 
-    # Compulsory bytes (SURVEY.md §8 d); the gradient adds its 8 B per
-    # effective parameter written.
-    bytes_per_launch = info.bytes_jacobian_eval + (8 * prog.num_effective_parameters
-                                                   if args.gradient else 0)
-    if args.mode == "residual":
-        bytes_per_launch = info.bytes_residual_eval
-    elif args.mode == "spmv":
-        # J read twice, p/J p/J^T J p vectors; kernel_ms (events around the
-        # evaluate launches only) does not apply, the step time does
-        bytes_per_launch = 2 * 8 * prog.num_jacobian_values
-    elif args.mode == "cgnr":
-        # the normal operator's compulsory bytes: J once, p, D and y
-        bytes_per_launch = 8 * prog.num_jacobian_values + 4 * 8 * prog.num_effective_parameters
-    elif args.mode == "candidate":
-        # the timed kernel is the cost-only evaluation (no residual stores);
-        # Plus is in ms_per_step, not in kernel_ms_avg
-        bytes_per_launch = info.bytes_residual_eval - 8 * prog.num_residuals
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    weak = args.scaling == "weak" or world == 1
-    value = (world if weak else 1) * args.steps / elapsed
+        def leg(name, fn, nbytes, steps, what):
+            e, k, kmax = run_leg(fn, steps, 2)
+            tb = reduce_sum(nbytes)
+            ach = tb / world / (kmax * 1e-3) / 1e9
+            secondary[name] = {"value": units * steps / e, "unit": "evals/s",
+                               "ms_per_step": e / steps * 1e3, "steps": steps,
+                               "kernel_ms_avg": k, "kernel_ms_avg_max_rank": kmax,
+                               "algorithmic_bytes_per_launch": nbytes,
+                               "achieved_GBps": ach, "frac": ach / PEAK_HBM_GBPS, "what": what}
+
+        if not args.gradient:
+            leg("gradient", lambda: se.evaluate(residuals=True, jacobian=True, gradient=True),
+                info.bytes_jacobian_eval + 8 * ne, ks,
+                "residuals + Jacobian + gradient J^T r + cost (fused deterministic gradient, "
+                "gradient_mode 0; what TrustRegionMinimizer requests); bytes add 8 per "
+                "effective parameter")
+        leg("residual_only", lambda: se.evaluate(residuals=True, jacobian=False, gradient=False),
+            info.bytes_residual_eval, ks, "residuals + cost (trust-region candidate evaluation)")
+        hres, hjac = se.host_buffers()
+
+        def host_step():
+            se.evaluate(residuals=True, jacobian=True, gradient=False)
+            se.copy_strips_to_host(hres, hjac)
+
+        e, _, _ = run_leg(host_step, args.host_steps, 1)
+        d2h = se.d2h_bytes()
+        secondary["host_strips"] = {
+            "value": units * args.host_steps / e, "unit": "evals/s",
+            "ms_per_step": e / args.host_steps * 1e3, "steps": args.host_steps,
+            "d2h_bytes_per_rank": d2h, "d2h_GBps_per_rank": d2h * args.host_steps / e / 1e9,
+            "what": "evaluation + D2H of each rank's residual and Jacobian strips into pinned "
+                    "host memory every step (the reference's seam; PCIe-inclusive, not the "
+                    "headline value)"}
+        del hres, hjac
+
     out = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-            cpu = cpu_baseline(args, threads)
+        if arrays is not None:
+            share = len(os.sched_getaffinity(0))
+            omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+            threads = args.cpu_threads or (min(omp, share) if omp > 0 else share)
+            cpu = cpu_baseline(args, arrays, threads)
         traffic = None
         pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}_{args.loss}_{args.format}.json")
-        if os.path.exists(pmc_path):
+        if world == 1 and args.mode == "jacobian" and not args.gradient and os.path.exists(pmc_path):
             with open(pmc_path) as fh:
-                pmc = json.load(fh)
-            traffic = pmc.get("hbm_bytes_per_launch")
-        C_, P_, O_ = bal.CONFIGS[args.config]
+                traffic = json.load(fh).get("hbm_bytes_per_launch")
+        C_, P_, O_ = counts
+        sh = se.shard
         out = {
             "metric": METRIC if args.mode == "jacobian" else
                       f"{args.mode} evaluations/sec on BAL {args.config} (not the headline)",
@@ -306,7 +410,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if weak else "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (BAL-shaped: exact header counts, seeded generator)",
@@ -319,10 +423,16 @@ def main():
                                "cgnr": "J^T J p + D^2 p (one pass)"}[args.mode]
                             + f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
-                "blocks_per_rank": shard_info["blocks"],
-                "parallelism": ("replica shards per rank" if weak and world > 1 else
-                                "point-bucket block sharding" if world > 1 else "single GPU"),
-                "strip_rank0": shard_info["strip"],
+                "blocks_rank0": sh.blocks[1] - sh.blocks[0],
+                "parallelism": ("single GPU" if world == 1 else
+                                f"point-bucket block sharding x{world}" if strong else
+                                f"replica shards x{world}"),
+                "exchange": (None if world == 1 else
+                             f"all-reduce of the cost{' and camera gradient rows' if args.gradient else ''}"
+                             f" over {'RCCL' if backend == 'nccl' else backend}"),
+                "rehearsal": (f"{world} ranks on {ndev} GPU(s), gloo" if rehearsal else None),
+                "strip_rank0": {"residuals": list(sh.residual_strip),
+                                "jacobian": [[g, g + n] for _, g, n in sh.jacobian_strips()]},
             },
             "roofline": {
                 "bound": "hbm",
@@ -331,14 +441,18 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBPS,
                 "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_launch": tot_bytes / world,
                 "kernel_ms_avg": kernel_ms,
                 "kernel_ms_avg_max_rank": kernel_ms_max,
-                "kernel": "cse::EvaluateAffineChunks<SnavelyKind, loss, jacobian, layout, ...>",
-                "traffic_source": "profiles/pmc_<config>_<loss>_<format>.json (rocprofv3 FETCH_SIZE/WRITE_SIZE)",
+                "kernel": f"cse::EvaluateAffineChunks{'Fused' if args.gradient else ''}"
+                          f"<SnavelyKind, {args.loss}, {args.format}> (+ repack"
+                          f"{', gradient tail' if args.gradient else ''})",
+                "per": "GPU (bytes of all ranks / N over the slowest rank's kernel time)",
+                "traffic_source": "profiles/pmc_<config>_<loss>_<format>.json (rocprofv3 "
+                                  "FETCH_SIZE/WRITE_SIZE of the same kernel)",
             },
+            "secondary": secondary,
             "cpu_baseline": cpu,
-            "host_copy": host_copy,
             "speedup_vs_cpu": (value / world / cpu["value"]) if cpu else None,
             "build_s": build_s,
             "reference_published": {"value": 0.6455, "unit": "evals/s",
@@ -346,9 +460,9 @@ def main():
                                             "README.md:189 (not the same metric)"},
         }
         print(json.dumps(out), flush=True)
-    ev.close()
+    se.close()
     if world > 1:
-        dist.barrier()
+        barrier()
         dist.destroy_process_group()
     return out
 

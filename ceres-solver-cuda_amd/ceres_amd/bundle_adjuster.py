@@ -147,6 +147,12 @@ def solve(args):
         raise SystemExit("initial evaluation failed")
     initial_cost = float(cost.item())
     radius = args.initial_trust_region_radius
+    # LevenbergMarquardtStrategy (levenberg_marquardt_strategy.cc:157-170):
+    # a rejected step divides the radius by decrease_factor and doubles it;
+    # an accepted one resets it to 2.
+    decrease_factor = 2.0
+    max_radius = 1e16  # Solver::Options::max_trust_region_radius
+    min_relative_decrease = 1e-3  # Solver::Options::min_relative_decrease
     rows = []
     D = None
     for it in range(args.num_iterations):
@@ -173,15 +179,20 @@ def solve(args):
         ev.right_multiply_device(jac.data_ptr(), dx.data_ptr(), Jdx.data_ptr())
         model = float(-(torch.dot(g, dx) + 0.5 * torch.dot(Jdx, Jdx)).item())
         rho = (old_cost - new_cost) / model if model > 0 else -1.0
-        accepted = new_cost < old_cost
+        # TrustRegionMinimizer::IsStepSuccessful: relative decrease above
+        # min_relative_decrease (trust_region_minimizer.cc).
+        accepted = ok and rho > min_relative_decrease
         rows.append((it, old_cost, new_cost, float(g.norm().item()), float(dx.norm().item()),
                      radius, cg_iters, accepted))
         if accepted:
             x.copy_(cand)
-            timed("Jacobian & residual evaluation", jacobian_eval)
-            radius = radius / max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3)
+            if timed("Jacobian & residual evaluation", jacobian_eval) != 0:
+                raise SystemExit(f"iteration {it}: Jacobian evaluation at the accepted point failed")
+            radius = min(max_radius, radius / max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3))
+            decrease_factor = 2.0
         else:
-            radius = radius / 2.0
+            radius = radius / decrease_factor
+            decrease_factor *= 2.0
     ev.close()
     print("iter      cost      cost_new   |gradient|    |step|    tr_radius  ls_iter  accepted")
     for it, c0, c1, gn, sn, rad, li, acc in rows:

@@ -40,6 +40,16 @@ class oracle_sizes(C.Structure):
 _lib = None
 
 
+def use_library(path):
+    """Load `path` (another build of oracle.cpp, e.g. the -march=native CPU
+    baseline of `make native`) instead of build/liboracle.so.  Must be
+    called before the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("liboracle already loaded from " + LIB_PATH)
+    LIB_PATH = os.path.abspath(path)
+
+
 def lib():
     global _lib
     if _lib is None:

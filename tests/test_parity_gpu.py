@@ -81,7 +81,9 @@ def test_problem_1778_compressed_row_huber(gpu):
                                  format=ca.COMPRESSED_ROW)
     ref = oracle_eval(prog, threads=16)
     got, _ = gpu_eval(prog)
-    assert_parity(got, ref, "problem-1778")
+    rep = {}
+    assert_parity(got, ref, "problem-1778", report=rep)
+    print("problem-1778 CRS Huber parity:", rep)
 
 
 @pytest.mark.parametrize("combo", range(8))
@@ -334,10 +336,14 @@ def test_problem_13682_full_size(gpu):
     prog = bal.synthetic_program("problem-13682-4456117", loss=ca.Loss.huber(1.0))
     O_ = prog.num_residual_blocks
     assert prog.num_jacobian_values == 24 * O_
-    got, info = gpu_eval(prog, residuals=True, gradient=False, jacobian=True)
-    assert info.num_affine_groups == 1
-    ref = oracle_eval(prog, threads=16, residuals=True, gradient=False, jacobian=True)
-    assert_parity(got, ref, "problem-13682")
+    # The gradient comes from the fused deterministic path (gradient_mode 0),
+    # as in a trust-region Jacobian evaluation.
+    got, info = gpu_eval(prog, residuals=True, gradient=True, jacobian=True)
+    assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
+    ref = oracle_eval(prog, threads=16, residuals=True, gradient=True, jacobian=True)
+    rep = {}
+    assert_parity(got, ref, "problem-13682", report=rep)
+    print("problem-13682 BSM Huber parity:", rep)
 
 
 def test_gradient_post_pass_deterministic_and_agrees_with_atomics(gpu):

@@ -1,0 +1,51 @@
+#!/bin/bash
+# One gpurun session made of named steps, each under its own time limit:
+#   tools/gpu_steps.sh TAG STEP [STEP ...]
+# Steps:
+#   tests      pytest -m "gpu and not slow"
+#   slow       pytest -m slow -s (full-size parity, prints max_rel_err)
+#   bench      bench.py (the driver's default line)
+#   bench2     bench.py --gpus 2 (a 2-rank rehearsal of configs[4] on one GPU)
+#   prof       rocprofv3 --kernel-trace --stats of a short bench.py run
+#   ab:V,V,..  tools/ab_bench.py over tuning variants (lib/libcse_tuning.so)
+#   py:FILE    python -u FILE (a tools/ script)
+# Output goes to gpurun_out/TAG/.  A step that ends with a fault, an abort,
+# a segfault or a time limit stops the session (no further GPU step).
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 3
+export CSE_BAL_CACHE=/tmp/cse_bal_cache
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
+for s in "$@"; do
+  case "$s" in
+    tests)  timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -v --timeout 120 \
+              --timeout-method thread > "$OUT/pytest_gpu.txt" 2>&1; rc=$?
+            tail -3 "$OUT/pytest_gpu.txt"; grep -E "FAILED|Error" "$OUT/pytest_gpu.txt" | head -20 ;;
+    slow)   timeout -k 10 900 python -u -m pytest tests -m slow -x -v -s --timeout 600 \
+              --timeout-method thread > "$OUT/pytest_slow.txt" 2>&1; rc=$?
+            grep -E "parity:|passed|failed|FAILED" "$OUT/pytest_slow.txt" | tail -8 ;;
+    bench)  timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+            tail -c 3000 "$OUT/bench.json"; tail -5 "$OUT/bench.err" ;;
+    bench2) timeout -k 10 600 python -u bench.py --gpus 2 --steps 10 --no-cpu-baseline \
+              > "$OUT/bench2.json" 2> "$OUT/bench2.err"; rc=$?
+            tail -c 2500 "$OUT/bench2.json"; tail -5 "$OUT/bench2.err" ;;
+    prof)   mkdir -p "$OUT/prof"
+            timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+              --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 10 \
+              --warmup 2 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$?
+            tail -c 1500 "$OUT/prof_bench.json" ;;
+    ab:*)   timeout -k 10 600 python -u tools/ab_bench.py --variants "${s#ab:}" --rounds 3 \
+              --steps 20 --out "$OUT/ab.json" > "$OUT/ab.txt" 2>&1; rc=$?
+            tail -12 "$OUT/ab.txt" ;;
+    py:*)   f=${s#py:}; b=$(basename "$f" .py)
+            timeout -k 10 600 python -u "$f" > "$OUT/$b.txt" 2>&1; rc=$?
+            tail -20 "$OUT/$b.txt" ;;
+    *)      echo "unknown step $s"; rc=2 ;;
+  esac
+  echo "== step $s rc=$rc"
+  if [ "$rc" -ne 0 ]; then
+    case "$s" in tests|slow) fatal "$rc" && exit "$rc" ;; *) exit "$rc" ;; esac
+  fi
+done
+exit 0
