@@ -249,8 +249,15 @@ void LaunchBounded(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 template <int L>
-LaunchFn TuningVariant(int v) {
+LaunchFn TuningVariant(int v, bool jac) {
   using K = cse::SnavelyKind;
+  if (!jac) {  // residual / cost-only kernels
+    switch (v) {
+      case 1: return &LaunchChunks<K, L, false, false, 2, cse::Tune<1, true>>;
+      case 2: return &LaunchChunks<K, L, false, false, 2, cse::Tune<2, true>>;
+      default: return nullptr;
+    }
+  }
   switch (v) {
     case 1: return &LaunchChunks<K, L, true, false, 2, cse::Tune<1, true>>;
     case 2: return &LaunchChunks<K, L, true, false, 2, cse::Tune<2, true>>;
@@ -267,11 +274,11 @@ LaunchFn TuningPick(int kind, int loss, bool jac, int policy, bool dma) {
   // Read at every launch, so that one process can A/B the variants.
   const char* e = getenv("CSE_TUNE_VARIANT");
   const int v = e ? atoi(e) : 0;
-  if (v <= 0 || kind != CSE_FUNCTOR_SNAVELY_2_9_3 || !jac || policy != kAffinePacked || !dma)
+  if (v <= 0 || kind != CSE_FUNCTOR_SNAVELY_2_9_3 || policy != kAffinePacked || !dma)
     return nullptr;
   switch (loss) {
-    case CSE_LOSS_HUBER: return TuningVariant<cse::kLossHuber>(v);
-    case CSE_LOSS_TRIVIAL: return TuningVariant<cse::kLossTrivial>(v);
+    case CSE_LOSS_HUBER: return TuningVariant<cse::kLossHuber>(v, jac);
+    case CSE_LOSS_TRIVIAL: return TuningVariant<cse::kLossTrivial>(v, jac);
     default: return nullptr;
   }
 }

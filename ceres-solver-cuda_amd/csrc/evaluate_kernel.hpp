@@ -338,7 +338,10 @@ struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
 };
-using ShippedTune = Tune<>;
+// Shipped: no priority changes.  kPrio 2 was 1.5-2 % faster with the
+// library sincos and divisions (profiles/round2/s1, s3c) and 2 % slower
+// once the functor's FP64 work shrank (profiles/round2/s3d).
+using ShippedTune = Tune<0, true>;
 
 // The hot kernel: one 64-block chunk per wave, every output store issued
 // back to back at the very end of the wave (see the store primitives in

@@ -8,6 +8,8 @@
 #ifndef CSE_FUNCTORS_HPP_
 #define CSE_FUNCTORS_HPP_
 
+#include <type_traits>
+
 #include "jet.hpp"
 
 namespace cse {
@@ -71,8 +73,15 @@ CSE_HD void QuaternionRotatePoint(const T q[4], const T pt[3], T out[3]) {
 // distortion (examples/snavely_reprojection_error.h:58-93).
 template <bool kDistortion, typename T>
 CSE_HD void Project(const T p[3], const T& focal, const T* l, const double* obs, T* r) {
-  const T xp = -p[0] / p[2];
-  const T yp = -p[1] / p[2];
+  T xp, yp;
+  if constexpr (std::is_same<T, double>::value) {
+    const double neg_inv = -1.0 / p[2];  // one division for both coordinates
+    xp = p[0] * neg_inv;
+    yp = p[1] * neg_inv;
+  } else {  // Jet division already shares 1 / p[2].a
+    xp = -p[0] / p[2];
+    yp = -p[1] / p[2];
+  }
   if constexpr (kDistortion) {
     const T r2 = xp * xp + yp * yp;
     const T distortion = 1.0 + r2 * (l[0] + l[1] * r2);

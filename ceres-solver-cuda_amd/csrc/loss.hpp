@@ -26,10 +26,13 @@ CSE_HD void EvaluateLoss(const LossParams& lp, double s, double rho[3]) {
   if constexpr (kLoss == kLossHuber) {
     const double a = lp.a, b = a * a;
     if (s > b) {
+      // loss_function_cuda.h:72-87 with one division: 1/r serves rho1 and
+      // rho2 = -rho1 / (2 s) = -0.5 rho1 / r^2.
       const double r = sqrt(s);
+      const double r_inv = 1.0 / r;
       rho[0] = 2.0 * a * r - b;
-      rho[1] = fmax(DBL_MIN, a / r);
-      rho[2] = -rho[1] / (2.0 * s);
+      rho[1] = fmax(DBL_MIN, a * r_inv);
+      rho[2] = -0.5 * rho[1] * (r_inv * r_inv);
     } else {
       rho[0] = s;
       rho[1] = 1.0;

@@ -88,4 +88,25 @@ int jet_ops_run(const double* x, const double* y, const double* z, double s, dou
   return kResults;
 }
 
+// sin and cos of n arguments through cse::SinCos, 64 per wave: the
+// library's reduction-free polynomial serves waves whose arguments are all
+// within pi/4, the library sincos every other wave.
+__global__ void SinCosKernel(const double* x, int n, double* s, double* c) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  cse::SinCos(x[i], s + i, c + i);
+}
+
+int sincos_run(const double* x, int n, double* s, double* c) {
+  double* d = nullptr;
+  if (hipMalloc(&d, 3 * (size_t)n * sizeof(double)) != hipSuccess) return -1;
+  bool ok = hipMemcpy(d, x, n * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+  hipLaunchKernelGGL(SinCosKernel, dim3((n + 255) / 256), dim3(256), 0, 0, d, n, d + n, d + 2 * n);
+  ok = ok && hipGetLastError() == hipSuccess &&
+       hipMemcpy(s, d + n, n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess &&
+       hipMemcpy(c, d + 2 * n, n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipFree(d);
+  return ok ? n : -1;
+}
+
 }  // extern "C"

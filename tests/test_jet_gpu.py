@@ -113,3 +113,35 @@ def test_device_jet_matches_reference_formulas(gpu):
         if not all(almost_equal(g, e) for g, e in zip(got, exp)):
             bad.append((names[i] if i < len(names) else i, got, exp))
     assert not bad, bad
+
+
+def test_device_sincos_polynomial_and_library_paths(gpu):
+    """cse::SinCos (jet.hpp): the reduction-free polynomial on waves whose
+    arguments all lie in [-pi/4, pi/4], the library sincos on the others.
+    Both within 2 ulp of the host libm on a dense sweep, on the ends of the
+    interval, on tiny and signed-zero arguments, and on waves that mix one
+    large angle into small ones (those must take the library path)."""
+    import numpy as np
+    lib = C.CDLL(LIB)
+    lib.sincos_run.restype = C.c_int
+    lib.sincos_run.argtypes = [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double),
+                               C.POINTER(C.c_double)]
+    q = math.pi / 4
+    small = np.concatenate([np.linspace(-q, q, 64 * 2000), [q, -q, np.nextafter(q, 0), 1e-300,
+                                                             -1e-300, 0.0, 5e-9, -3e-5] * 8])
+    small = small[: len(small) // 64 * 64]
+    mixed = np.random.default_rng(3).uniform(-q, q, 64 * 64)
+    mixed[::64] = np.random.default_rng(4).uniform(1.0, 40.0, 64)  # one big angle per wave
+    big = np.random.default_rng(5).uniform(-1e4, 1e4, 64 * 64)
+    x = np.ascontiguousarray(np.concatenate([small, mixed, big]))
+    n = len(x)
+    s = np.empty(n)
+    c = np.empty(n)
+    p = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    assert lib.sincos_run(p(x), n, p(s), p(c)) == n
+    ref_s = np.array([math.sin(v) for v in x])
+    ref_c = np.array([math.cos(v) for v in x])
+    ulp_s = np.spacing(np.abs(ref_s)) + 5e-324
+    ulp_c = np.spacing(np.abs(ref_c)) + 5e-324
+    assert np.max(np.abs(s - ref_s) / ulp_s) <= 2.0, np.max(np.abs(s - ref_s) / ulp_s)
+    assert np.max(np.abs(c - ref_c) / ulp_c) <= 2.0, np.max(np.abs(c - ref_c) / ulp_c)

@@ -23,7 +23,10 @@ import numpy as np  # noqa: E402
 
 from ceres_amd import _cse  # noqa: E402
 
-_cse.use_library(os.path.join(REPO, "ceres-solver-cuda_amd", "lib", "libcse_tuning.so"))
+_LIB = os.path.join(REPO, "ceres-solver-cuda_amd", "lib", "libcse_tuning.so")
+if "--lib" in sys.argv:  # another tuning build of the same ABI (e.g. the previous commit's)
+    _LIB = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+_cse.use_library(_LIB)
 
 import ceres_amd as ca  # noqa: E402
 from ceres_amd import bal  # noqa: E402
@@ -37,6 +40,8 @@ def main():
     ap.add_argument("--config", default="problem-13682-4456117")
     ap.add_argument("--loss", default="huber")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", default=None, help="tuning library to load (default lib/libcse_tuning.so)")
+    ap.add_argument("--mode", default="jacobian", choices=["jacobian", "residual", "cost"])
     args = ap.parse_args()
     import torch
     variants = [int(v) for v in args.variants.split(",")]
@@ -58,10 +63,13 @@ def main():
         for v in variants:
             os.environ["CSE_TUNE_VARIANT"] = str(v)
             ev = ca.Evaluator(prog, device=0, profile=True, stream=stream.cuda_stream)
-            bytes_ = ev.info().bytes_jacobian_eval
+            info = ev.info()
+            bytes_ = {"jacobian": info.bytes_jacobian_eval, "residual": info.bytes_residual_eval,
+                      "cost": info.bytes_residual_eval - 8 * prog.num_residuals}[args.mode]
+            rp = res.data_ptr() if args.mode != "cost" else None
+            jp = jac.data_ptr() if args.mode == "jacobian" else None
             for _ in range(3):
-                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None,
-                                   jac.data_ptr())
+                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, None, jp)
             assert ev.wait() == 0
             if rnd == 0:
                 h = hashlib.sha1()
@@ -76,8 +84,7 @@ def main():
                 print(f"# variant {v}: outputs {'identical' if same else 'DIFFER'}", flush=True)
             ev.reset_kernel_stats()
             for _ in range(args.steps):
-                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), None,
-                                   jac.data_ptr())
+                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, None, jp)
             assert ev.wait() == 0
             _, total, n = ev.kernel_stats()
             ev.close()
@@ -87,7 +94,7 @@ def main():
                   f"frac {bytes_ / ms / 1e6 / 8000:.3f}", flush=True)
     summary = {v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                    "frac_median": bytes_ / float(np.median(t)) / 1e6 / 8000} for v, t in times.items()}
-    print(json.dumps(summary))
+    print(json.dumps({"mode": args.mode, "summary": summary}))
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"config": args.config, "loss": args.loss, "times_ms": times,

@@ -35,9 +35,32 @@ for s in "$@"; do
               --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 10 \
               --warmup 2 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$?
             tail -c 1500 "$OUT/prof_bench.json" ;;
-    ab:*)   timeout -k 10 600 python -u tools/ab_bench.py --variants "${s#ab:}" --rounds 3 \
-              --steps 20 --out "$OUT/ab.json" > "$OUT/ab.txt" 2>&1; rc=$?
-            tail -12 "$OUT/ab.txt" ;;
+    pmc:*)  # pmc:MODE[:extra bench args with commas]: one rocprofv3 --pmc pass per
+            # counter group (MI355X_MICROARCH.md block limits), then a summary
+            m=${s#pmc:}; mode=${m%%:*}; extra=""; [ "$m" != "$mode" ] && extra=$(echo "${m#*:}" | tr ',' ' ')
+            P="$OUT/pmc_$mode"; mkdir -p "$P"; rc=0
+            rocprofv3 -L > "$P/counters_list.txt" 2>&1 || true
+            i=0
+            for group in "FETCH_SIZE" "WRITE_SIZE" \
+                "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU" \
+                "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+                "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE TCC_HIT_sum TCC_MISS_sum" \
+                "TA_BUSY_avr TD_BUSY_avr" "SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS"; do
+              i=$((i+1))
+              timeout -s KILL 120 rocprofv3 --pmc $group -d "$P/g$i" -o run --output-format csv -- \
+                python3 bench.py --no-cpu-baseline --no-secondary --steps 10 --warmup 2 --mode $mode $extra \
+                > "$P/g$i.log" 2>&1 || echo "group $i ($group) rc=$?" >> "$P/errors.txt"
+            done
+            for d in "$P"/g*; do [ -d "$d" ] && python3 tools/pmc_summary.py "$d" Evaluate --json "$P/summary.json" > /dev/null; done
+            cat "$P/summary.json"; cat "$P/errors.txt" 2>/dev/null ;;
+    ab*:*)  # ab:V,V,.. (Jacobian) or abres:V,.. / abcost:V,.. (residual / cost-only);
+            # abprev:/abprevres: the same on lib/libcse_prev_tuning.so
+            kind=${s%%:*}; mode=jacobian; lib=""; tag=$kind
+            case "$kind" in *res) mode=residual ;; *cost) mode=cost ;; esac
+            case "$kind" in abprev*) lib="--lib ceres-solver-cuda_amd/lib/libcse_prev_tuning.so" ;; esac
+            timeout -k 10 600 python -u tools/ab_bench.py --variants "${s#*:}" --rounds 3 \
+              --steps 20 --mode $mode $lib --out "$OUT/$tag.json" > "$OUT/$tag.txt" 2>&1; rc=$?
+            tail -6 "$OUT/$tag.txt" ;;
     py:*)   f=${s#py:}; b=$(basename "$f" .py)
             timeout -k 10 600 python -u "$f" > "$OUT/$b.txt" 2>&1; rc=$?
             tail -20 "$OUT/$b.txt" ;;
