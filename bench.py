@@ -73,12 +73,13 @@ def parse():
     ap.add_argument("--gradient-mode", type=int, default=0, choices=[0, 1, 2],
                     help="cse_options.gradient_mode: 0 fused (default), 1 post-pass, 2 atomics")
     ap.add_argument("--mode", default="jacobian",
-                    choices=["jacobian", "residual", "candidate", "spmv", "cgnr"],
+                    choices=["jacobian", "residual", "candidate", "spmv", "cgnr", "schur"],
                     help="jacobian: residual+Jacobian evaluation (the headline metric); "
                          "residual: residuals+cost only; candidate: the trust-region candidate "
                          "step, Plus(x, delta) then cost-only evaluation "
                          "(trust_region_minimizer.cc:770-788); spmv: one CGNR iteration's "
-                         "products J p and J^T (J p); cgnr: the one-pass normal operator")
+                         "products J p and J^T (J p); cgnr: the one-pass normal operator; "
+                         "schur: one product with the implicit Schur complement (cse_schur_multiply)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the gradient / residual-only / host-strip legs")
     ap.add_argument("--secondary-steps", type=int, default=20)
@@ -298,6 +299,21 @@ def main():
         dvec = torch.full((ne,), 0.5, dtype=f64, device=dev)
         jp = torch.zeros(prog.num_residuals, dtype=f64, device=dev)
         jtjp = torch.zeros(ne, dtype=f64, device=dev)
+    if args.mode == "schur":
+        se.evaluate(residuals=True, jacobian=True, gradient=False)
+        e_cols, f_cols = ev.schur_structure()
+        ne = prog.num_effective_parameters
+        dvec = torch.full((ne,), 0.5, dtype=f64, device=dev)
+        bvec = -se.residuals
+        srhs = torch.empty(f_cols, dtype=f64, device=dev)
+        torch.cuda.synchronize(dev)
+        t_init = time.perf_counter()
+        ev.schur_init_device(se.jacobian.data_ptr(), dvec.data_ptr(), bvec.data_ptr(),
+                             srhs.data_ptr(), ca._cse.SCHUR_JACOBI)
+        torch.cuda.synchronize(dev)
+        schur_init_ms = (time.perf_counter() - t_init) * 1e3
+        sx = torch.ones(f_cols, dtype=f64, device=dev)
+        sy = torch.empty(f_cols, dtype=f64, device=dev)
     if args.mode == "candidate":
         delta = torch.full((prog.num_effective_parameters,), 1e-6, dtype=f64, device=dev)
         cand = torch.empty_like(se.state)
@@ -312,6 +328,8 @@ def main():
             ev.evaluate_device(cand.data_ptr(), se.cost.data_ptr(), None, None, None)
             if se.exchange:
                 se._all_reduce(se.cost)
+        elif args.mode == "schur":
+            ev.schur_multiply_device(sx.data_ptr(), sy.data_ptr())
         elif args.mode == "cgnr":  # one pass: J^T J p + D^2 p (cse_cgnr_multiply)
             ev.cgnr_multiply_device(se.jacobian.data_ptr(), dvec.data_ptr(), pvec.data_ptr(),
                                     jtjp.data_ptr())
@@ -320,11 +338,12 @@ def main():
             ev.left_multiply_device(se.jacobian.data_ptr(), jp.data_ptr(), jtjp.data_ptr())
 
     elapsed, kernel_ms, kernel_ms_max = run_leg(step, args.steps, args.warmup)
-    if args.mode in ("spmv", "cgnr"):  # no evaluate launches in the loop: the step time
+    if args.mode in ("spmv", "cgnr", "schur"):  # no evaluate launches in the loop: the step time
         kernel_ms = kernel_ms_max = elapsed / args.steps * 1e3
 
     # Compulsory bytes per launch on this rank (SURVEY.md §8 d).
     ne, nres, nj = prog.num_effective_parameters, prog.num_residuals, prog.num_jacobian_values
+    npt = se.shard.points[1] - se.shard.points[0]
     bytes_launch = {
         "jacobian": info.bytes_jacobian_eval + (8 * ne if args.gradient else 0),
         "residual": info.bytes_residual_eval,
@@ -332,6 +351,8 @@ def main():
         "candidate": info.bytes_residual_eval - 8 * nres,
         "spmv": 2 * 8 * nj,  # J read twice (vectors are small next to it)
         "cgnr": 8 * nj + 4 * 8 * ne,  # J once, p, D and y
+        # J once, the block ids, (E^T E + D_e^2)^-1 per point, x, D_f and y
+        "schur": 8 * nj + 8 * prog.num_residual_blocks + 48 * npt + 3 * 8 * (ne - 3 * npt),
     }[args.mode]
     def reduce_sum(v):
         if world == 1:
@@ -420,7 +441,8 @@ def main():
                             + {"jacobian": "residual+Jacobian", "residual": "residual+cost",
                                "candidate": "Plus + cost-only",
                                "spmv": "J p + J^T (J p)",
-                               "cgnr": "J^T J p + D^2 p (one pass)"}[args.mode]
+                               "cgnr": "J^T J p + D^2 p (one pass)",
+                               "schur": "S p, implicit Schur complement"}[args.mode]
                             + f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
                 "blocks_rank0": sh.blocks[1] - sh.blocks[0],
@@ -452,6 +474,7 @@ def main():
                                   "FETCH_SIZE/WRITE_SIZE of the same kernel)",
             },
             "secondary": secondary,
+            "schur_init_ms": schur_init_ms if args.mode == "schur" else None,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / world / cpu["value"]) if cpu else None,
             "build_s": build_s,

@@ -51,6 +51,11 @@ FUNCTOR_SHAPES = {
     TEST_PARTIAL_OUTPUT_2_1: (2, (1,), 1),
 }
 
+# cse_schur_preconditioner
+SCHUR_IDENTITY = 0
+SCHUR_JACOBI = 1
+SCHUR_SCHUR_JACOBI = 2
+
 # cse_loss_kind
 LOSS_TRIVIAL = 0
 LOSS_HUBER = 1
@@ -132,6 +137,12 @@ SIGNATURES = {
     "cse_jacobian_right_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_jacobian_left_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_cgnr_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_schur_structure": (C.c_int, [C.c_void_p, P_i64, P_i64]),
+    "cse_schur_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_int]),
+    "cse_schur_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_schur_precondition": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_schur_back_substitute": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_destroy": (None, [C.c_void_p]),
     "cse_last_error": (C.c_char_p, []),
     "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),

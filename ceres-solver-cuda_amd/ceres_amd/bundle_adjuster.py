@@ -4,8 +4,10 @@ Mirrors the flow of examples/bundle_adjuster.cu.cc around the hot path:
 read a BAL file (or build a synthetic one), Normalize(), Perturb(), put the
 residual blocks in Schur order, and run Levenberg-Marquardt iterations
 whose every evaluation is the HIP evaluator and whose linear solve is a
-Jacobi-preconditioned CGNR on the device operator (no Jacobian value leaves
-HBM).  Prints a FullReport-style table of the evaluator timers
+preconditioned CG on the device's implicit Schur complement
+(--linear_solver iterative_schur, the reference benchmark's solver, with its
+jacobi / schur_jacobi / identity preconditioners) or on the normal equations
+(--linear_solver cgnr); no Jacobian value leaves HBM.  Prints a FullReport-style table of the evaluator timers
 (solver.cc: "Residual only evaluation", "Jacobian & residual evaluation",
 "Linear solver", "Plus").
 
@@ -46,6 +48,13 @@ def parse(argv=None):
     ap.add_argument("--max_linear_solver_iterations", type=int, default=500)
     ap.add_argument("--eta", type=float, default=1e-2, help="CG forcing tolerance")
     ap.add_argument("--initial_trust_region_radius", type=float, default=1e4)
+    ap.add_argument("--linear_solver", default="iterative_schur", choices=["iterative_schur", "cgnr"],
+                    help="iterative_schur (the reference benchmark's, README.md:143-184): PCG on "
+                         "the implicit Schur complement (cse_schur_*); cgnr: PCG on the normal "
+                         "equations (cse_cgnr_multiply)")
+    ap.add_argument("--preconditioner", default="jacobi",
+                    choices=["identity", "jacobi", "schur_jacobi"],
+                    help="iterative_schur's preconditioner (bundle_adjuster.cc default: jacobi)")
     return ap.parse_args(argv)
 
 
@@ -142,6 +151,46 @@ def solve(args):
             rz = rz_new
         return dx, it
 
+    if args.linear_solver == "iterative_schur":
+        e_cols, f_cols = ev.schur_structure()
+        pre = {"identity": ca._cse.SCHUR_IDENTITY, "jacobi": ca._cse.SCHUR_JACOBI,
+               "schur_jacobi": ca._cse.SCHUR_SCHUR_JACOBI}[args.preconditioner]
+        rhs = torch.empty(f_cols, dtype=f64, device=dev)
+        neg_r = torch.empty(m, dtype=f64, device=dev)
+
+    def schur_solve(lam):
+        # IterativeSchurComplementSolver (iterative_schur_complement_solver.cc:
+        # 63-170): the augmented system [J; sqrt(lam diag(J^T J))] dx = [-r; 0]
+        # reduced to S dx_f = rhs, PCG on S, then back substitution.
+        torch.neg(r, out=neg_r)
+        sqrt_lam_d = torch.sqrt(lam * D)
+        ev.schur_init_device(jac.data_ptr(), sqrt_lam_d.data_ptr(), neg_r.data_ptr(),
+                             rhs.data_ptr(), pre)
+        xf = torch.zeros(f_cols, dtype=f64, device=dev)
+        res = rhs.clone()
+        z = torch.zeros_like(res)
+        ev.schur_precondition_device(res.data_ptr(), z.data_ptr())
+        p = z.clone()
+        Ap = torch.empty_like(p)
+        rz = torch.dot(res, z)
+        bn = rhs.norm()
+        it = 0
+        for it in range(1, args.max_linear_solver_iterations + 1):
+            ev.schur_multiply_device(p.data_ptr(), Ap.data_ptr())
+            alpha = rz / torch.dot(p, Ap)
+            xf += alpha * p
+            res -= alpha * Ap
+            if res.norm() <= args.eta * bn:
+                break
+            z.zero_()
+            ev.schur_precondition_device(res.data_ptr(), z.data_ptr())
+            rz_new = torch.dot(res, z)
+            p = z + (rz_new / rz) * p
+            rz = rz_new
+        dx = torch.empty(n, dtype=f64, device=dev)
+        ev.schur_back_substitute_device(xf.data_ptr(), dx.data_ptr())
+        return dx, it
+
     status = timed("Jacobian & residual evaluation", jacobian_eval)
     if status != 0:
         raise SystemExit("initial evaluation failed")
@@ -164,7 +213,8 @@ def solve(args):
         ev.left_multiply_device(jac2.data_ptr(), ones.data_ptr(), D.data_ptr())
         D.clamp_(min=1e-6)
         del jac2
-        dx, cg_iters = timed("Linear solver", lambda: cgnr(1.0 / radius))
+        solver = schur_solve if args.linear_solver == "iterative_schur" else cgnr
+        dx, cg_iters = timed("Linear solver", lambda: solver(1.0 / radius))
         timed("Plus", lambda: ev.plus_device(x.data_ptr(), dx.data_ptr(), cand.data_ptr()))
 
         def cand_eval():

@@ -432,6 +432,36 @@ class Evaluator:
         return _cse.check(_cse.lib().cse_cgnr_multiply(self.handle, d_jacobian, d_D, d_x, d_y),
                           "cse_cgnr_multiply")
 
+    # ---- ITERATIVE_SCHUR (ImplicitSchurComplement on the device) ----------
+    def schur_structure(self):
+        """(num_cols_e, num_cols_f) of the Schur split; raises if the problem
+        does not have the structure (cse_schur_structure)."""
+        e, f = C.c_int64(), C.c_int64()
+        _cse.check(_cse.lib().cse_schur_structure(self.handle, C.byref(e), C.byref(f)),
+                   "cse_schur_structure")
+        return e.value, f.value
+
+    def schur_init_device(self, d_jacobian, d_D, d_b, d_rhs, preconditioner=_cse.SCHUR_JACOBI):
+        """ImplicitSchurComplement::Init(A, D, b) + the preconditioner; writes
+        the reduced right-hand side (num_cols_f) to d_rhs."""
+        return _cse.check(_cse.lib().cse_schur_init(self.handle, d_jacobian, d_D, d_b, d_rhs,
+                                                    int(preconditioner)), "cse_schur_init")
+
+    def schur_multiply_device(self, d_x, d_y):
+        """y = S x (ImplicitSchurComplement::RightMultiplyAndAccumulate)."""
+        return _cse.check(_cse.lib().cse_schur_multiply(self.handle, d_x, d_y),
+                          "cse_schur_multiply")
+
+    def schur_precondition_device(self, d_x, d_y):
+        """y += M^-1 x for the preconditioner chosen at init."""
+        return _cse.check(_cse.lib().cse_schur_precondition(self.handle, d_x, d_y),
+                          "cse_schur_precondition")
+
+    def schur_back_substitute_device(self, d_x, d_y):
+        """y = [(E^T E + D_e^2)^-1 E^T (b - F x); x] (BackSubstitute)."""
+        return _cse.check(_cse.lib().cse_schur_back_substitute(self.handle, d_x, d_y),
+                          "cse_schur_back_substitute")
+
     def plus_device(self, d_state, d_delta, d_out):
         """Device-pointer Plus on the evaluator's stream.  Async."""
         return _cse.check(_cse.lib().cse_plus_device(self.handle, d_state, d_delta, d_out),

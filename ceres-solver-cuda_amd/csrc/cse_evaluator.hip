@@ -22,7 +22,7 @@
 #include <vector>
 
 #include "../../include/cse.h"
-#include "operator_kernels.hpp"
+#include "schur_kernels.hpp"
 
 namespace {
 
@@ -342,6 +342,20 @@ struct cse_evaluator {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
   double last_ms = 0.0, total_ms = 0.0;
   int64_t launches = 0;
+  // The implicit Schur complement (cse_schur_*): structure found at create
+  // time, values and vectors bound by cse_schur_init.
+  struct Schur {
+    bool eligible = false;
+    bool duplicates = false;  // an e block sees one f block twice
+    int64_t e_cols = 0, f_cols = 0;
+    int64_t f_col_base = 0;   // f index of camera id = f_col_base + 9 id
+    int64_t nchunks = 0, nbig = 0;
+    DevBuf<int64_t> chunk_begin, big;
+    DevBuf<double> ete_inv, precond, partial;
+    bool ready = false;
+    int preconditioner = CSE_SCHUR_IDENTITY;
+    const double *jac = nullptr, *D = nullptr, *b = nullptr;
+  } schur;
 };
 
 namespace {
@@ -629,6 +643,73 @@ int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
                      dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, ga, ch);
   CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+// The implicit Schur complement's structure (cse_schur_*): one Snavely
+// group on the fused-gradient path with the BlockSparseMatrix layout, its
+// e blocks (slot 1, points) the leading columns [0, e_cols) and its f blocks
+// (slot 0, cameras) the rest, as ITERATIVE_SCHUR's elimination ordering puts
+// them (iterative_schur_complement_solver.cc:66-80).  The e-block runs are cut
+// into wave chunks of whole runs; longer runs are listed as big.
+int BuildSchurPlan(cse_evaluator* ev, const cse_problem_desc* d, hipStream_t s) {
+  auto& S = ev->schur;
+  S.eligible = false;
+  if (ev->groups.size() != 1 || d->num_groups != 1) return CSE_OK;
+  const Group& G = ev->groups[0];
+  if (!G.fuse_ok || G.policy != kAffinePacked || G.kind != CSE_FUNCTOR_SNAVELY_2_9_3 ||
+      !ev->has_layout || ev->num_constant > 0)
+    return CSE_OK;
+  const cse_residual_group& g = d->groups[0];
+  const int32_t* ids = g.parameter_block_ids;
+  const int64_t n = g.num_blocks;
+  int32_t pmin = ids[1], pmax = ids[1], cmin = ids[0], cmax = ids[0];
+  for (int64_t i = 0; i < n; ++i) {
+    pmin = std::min(pmin, ids[2 * i + 1]);
+    pmax = std::max(pmax, ids[2 * i + 1]);
+    cmin = std::min(cmin, ids[2 * i]);
+    cmax = std::max(cmax, ids[2 * i]);
+  }
+  const int64_t e_lo = G.delta_base[1] + 3LL * pmin, e_hi = G.delta_base[1] + 3LL * pmax + 3;
+  const int64_t f_lo = G.delta_base[0] + 9LL * cmin, f_hi = G.delta_base[0] + 9LL * cmax + 9;
+  if (e_lo < 0 || f_lo != e_hi || f_hi != ev->num_effective || e_lo != 0) return CSE_OK;
+  S.e_cols = e_hi;
+  S.f_cols = f_hi - f_lo;
+  S.f_col_base = G.delta_base[0] - S.e_cols;
+  // One pass over the runs of equal e block: small runs are packed into
+  // chunks of at most a wave ([begin, end) pairs; chunks never straddle a
+  // big run), big runs listed on their own.
+  std::vector<int64_t> ranges, big;
+  std::vector<int32_t> cams;
+  bool dup = false;
+  int64_t run_start = 0, chunk_lo = 0;
+  for (int64_t i = 1; i <= n; ++i) {
+    if (i < n && ids[2 * i + 1] == ids[2 * (i - 1) + 1]) continue;
+    const int64_t len = i - run_start;  // the run [run_start, i)
+    cams.assign(len, 0);
+    for (int64_t k = 0; k < len; ++k) cams[k] = ids[2 * (run_start + k)];
+    std::sort(cams.begin(), cams.end());
+    dup = dup || std::adjacent_find(cams.begin(), cams.end()) != cams.end();
+    if (len > cse::kWave) {
+      if (run_start > chunk_lo) ranges.insert(ranges.end(), {chunk_lo, run_start});
+      big.insert(big.end(), {run_start, i});
+      chunk_lo = i;
+    } else if (i - chunk_lo > cse::kWave) {
+      ranges.insert(ranges.end(), {chunk_lo, run_start});
+      chunk_lo = run_start;
+    }
+    run_start = i;
+  }
+  if (n > chunk_lo) ranges.insert(ranges.end(), {chunk_lo, n});
+  std::vector<int64_t>& begins = ranges;
+  S.duplicates = dup;
+  S.nchunks = (int64_t)begins.size() / 2;
+  S.nbig = (int64_t)big.size() / 2;
+  int rc;
+  if ((rc = S.chunk_begin.upload(begins.data(), begins.size(), s))) return rc;
+  if ((rc = S.big.upload(big.data(), big.size(), s))) return rc;
+  if (hipStreamSynchronize(s) != hipSuccess) return Fail(CSE_ERR_HIP, "Schur plan upload failed");
+  S.eligible = true;
   return CSE_OK;
 }
 
@@ -930,6 +1011,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       ok = owner[g.parameter_block_ids[2 * i + 1]] == 2 * gi + 1;
     G.fuse_ok = ok;
   }
+  if ((rc = BuildSchurPlan(ev, d, s))) return bail(rc);
   ev->res_covered = covered_res == d->num_residuals;
   ev->jac_covered = covered_jac == d->num_jacobian_values;
 
@@ -1156,6 +1238,194 @@ int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const 
     CSE_HIP(hipGetLastError());
     if ((rc = LaunchFusedGradTail(G, d_y, s))) return rc;
   }
+  return CSE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// ITERATIVE_SCHUR on the device (schur_kernels.hpp)
+// ---------------------------------------------------------------------------
+extern "C++" {
+namespace {
+
+cse::SchurArgs MakeSchurArgs(cse_evaluator* ev, const double* x, double* y) {
+  const Group& G = ev->groups[0];
+  const auto& S = ev->schur;
+  cse::SchurArgs a{};
+  a.n = G.n;
+  a.ids = G.ids.p;
+  a.jac = S.jac;
+  a.f_base = G.jac_base[0][0];
+  a.e_base = G.jac_base[1][0];
+  a.f_col_base = S.f_col_base;
+  a.e_col_base = G.delta_base[1];
+  a.e_cols = S.e_cols;
+  a.D = S.D;
+  a.b = S.b;
+  a.b_base = G.res_base;
+  a.x = x;
+  a.ete_inv = S.ete_inv.p;
+  a.contrib = G.gcontrib.p;
+  a.y = y;
+  a.chunk_begin = S.chunk_begin.p;
+  a.nchunks = S.nchunks;
+  a.big = S.big.p;
+  a.nbig = S.nbig;
+  return a;
+}
+
+template <int kMode>
+void LaunchSchurPass(const cse::SchurArgs& a, hipStream_t s) {
+  if (a.nchunks > 0)
+    hipLaunchKernelGGL((cse::SchurChunkKernel<9, kMode>),
+                       dim3((unsigned)((a.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
+                       dim3(cse::kBlockThreads), 0, s, a);
+  if (a.nbig > 0)
+    hipLaunchKernelGGL((cse::SchurBigKernel<9, kMode>),
+                       dim3((unsigned)((a.nbig + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
+                       dim3(cse::kBlockThreads), 0, s, a);
+}
+
+// y (f vector) += the per-f-block sums of the contributions just written.
+int SchurFTail(cse_evaluator* ev, double* y, hipStream_t s) {
+  const Group& G = ev->groups[0];
+  const Group::GradPlan& P = G.grad[0];
+  cse::GradArgs ga{};
+  ga.count = P.count;
+  ga.lo = P.lo;
+  ga.grad = y;
+  ga.delta_base = ev->schur.f_col_base;
+  const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
+  if (P.nchunks > 0)
+    hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
+                       dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
+                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch);
+  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
+                     dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, ga, ch);
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+int SchurCheck(cse_evaluator* ev, bool need_ready) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (!ev->schur.eligible)
+    return Fail(CSE_ERR_UNSUPPORTED,
+                "implicit Schur complement: needs one Snavely group on the affine BlockSparse path "
+                "with its points (slot 1) as the leading e columns and its cameras after them");
+  if (need_ready && !ev->schur.ready) return Fail(CSE_ERR_INVALID, "cse_schur_init has not run");
+  CSE_HIP(hipSetDevice(ev->device));
+  return CSE_OK;
+}
+
+}  // namespace
+}  // extern "C++"
+
+int cse_schur_structure(cse_evaluator* ev, int64_t* num_cols_e, int64_t* num_cols_f) {
+  int rc = SchurCheck(ev, false);
+  if (rc) return rc;
+  if (num_cols_e) *num_cols_e = ev->schur.e_cols;
+  if (num_cols_f) *num_cols_f = ev->schur.f_cols;
+  return CSE_OK;
+}
+
+int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                   const double* d_b, double* d_rhs, int preconditioner) {
+  int rc = SchurCheck(ev, false);
+  if (rc) return rc;
+  if (!d_jacobian_values || !d_b || !d_rhs) return Fail(CSE_ERR_INVALID, "null pointer");
+  auto& S = ev->schur;
+  if (preconditioner != CSE_SCHUR_IDENTITY && preconditioner != CSE_SCHUR_JACOBI &&
+      preconditioner != CSE_SCHUR_SCHUR_JACOBI)
+    return Fail(CSE_ERR_INVALID, "unknown preconditioner");
+  if (preconditioner == CSE_SCHUR_SCHUR_JACOBI && S.duplicates)
+    return Fail(CSE_ERR_UNSUPPORTED,
+                "SCHUR_JACOBI: an e block sees one f block in two residual blocks");
+  Group& G = ev->groups[0];
+  hipStream_t s = ev->stream;
+  if ((rc = S.ete_inv.ensure((size_t)2 * S.e_cols))) return rc;
+  if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
+  S.jac = d_jacobian_values;
+  S.D = d_D;
+  S.b = d_b;
+  S.preconditioner = preconditioner;
+  // M_p and rhs = F^T (b - E M E^T b).
+  CSE_HIP(hipMemsetAsync(d_rhs, 0, S.f_cols * sizeof(double), s));
+  cse::SchurArgs a = MakeSchurArgs(ev, nullptr, nullptr);
+  LaunchSchurPass<cse::kSchurInit>(a, s);
+  CSE_HIP(hipGetLastError());
+  if ((rc = SchurFTail(ev, d_rhs, s))) return rc;
+  if (preconditioner != CSE_SCHUR_IDENTITY) {
+    const Group::GradPlan& P = G.grad[0];
+    constexpr int T = cse::SymCount<9>();
+    if ((rc = S.partial.ensure((size_t)std::max<int64_t>(1, P.nchunks) * T))) return rc;
+    if ((rc = S.precond.ensure((size_t)81 * P.count))) return rc;
+    const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, S.partial.p, P.nchunks};
+    const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
+    if (P.nchunks > 0) {
+      if (preconditioner == CSE_SCHUR_SCHUR_JACOBI)
+        hipLaunchKernelGGL((cse::SchurBlockDiagKernel<9, true>), grid, dim3(cse::kBlockThreads), 0,
+                           s, a, P.perm.p, ch);
+      else
+        hipLaunchKernelGGL((cse::SchurBlockDiagKernel<9, false>), grid, dim3(cse::kBlockThreads), 0,
+                           s, a, P.perm.p, ch);
+    }
+    // d_off: D index of camera lo + p = e_cols + f index = e_cols + f_col_base + 9 (lo + p).
+    hipLaunchKernelGGL((cse::SchurBlockInvertKernel<9>), dim3((unsigned)((P.count + 63) / 64)),
+                       dim3(64), 0, s, ch, P.count, d_D,
+                       S.e_cols + S.f_col_base + 9LL * P.lo, S.precond.p);
+    CSE_HIP(hipGetLastError());
+  }
+  S.ready = true;
+  return CSE_OK;
+}
+
+int cse_schur_multiply(cse_evaluator* ev, const double* d_x, double* d_y) {
+  int rc = SchurCheck(ev, true);
+  if (rc) return rc;
+  if (!d_x || !d_y) return Fail(CSE_ERR_INVALID, "null pointer");
+  const auto& S = ev->schur;
+  hipStream_t s = ev->stream;
+  hipLaunchKernelGGL(cse::SchurDiagKernel,
+                     dim3((unsigned)((S.f_cols + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, S.D, S.e_cols, d_x, d_y, S.f_cols);
+  LaunchSchurPass<cse::kSchurMultiply>(MakeSchurArgs(ev, d_x, nullptr), s);
+  CSE_HIP(hipGetLastError());
+  return SchurFTail(ev, d_y, s);
+}
+
+int cse_schur_precondition(cse_evaluator* ev, const double* d_x, double* d_y) {
+  int rc = SchurCheck(ev, true);
+  if (rc) return rc;
+  if (!d_x || !d_y) return Fail(CSE_ERR_INVALID, "null pointer");
+  const auto& S = ev->schur;
+  hipStream_t s = ev->stream;
+  const unsigned grid = (unsigned)((S.f_cols + cse::kBlockThreads - 1) / cse::kBlockThreads);
+  if (S.preconditioner == CSE_SCHUR_IDENTITY) {  // IdentityPreconditioner: y += x
+    hipLaunchKernelGGL(cse::AxpyKernel, dim3(grid), dim3(cse::kBlockThreads), 0, s, d_x, d_y,
+                       S.f_cols);
+    CSE_HIP(hipGetLastError());
+    return CSE_OK;
+  }
+  const Group::GradPlan& P = ev->groups[0].grad[0];
+  // The cameras' f rows start at f index f_col_base + 9 lo.
+  const int64_t off = S.f_col_base + 9LL * P.lo;
+  hipLaunchKernelGGL((cse::SchurPrecondApplyKernel<9>), dim3(grid), dim3(cse::kBlockThreads), 0, s,
+                     S.precond.p, d_x + off, d_y + off, 9LL * P.count);
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+int cse_schur_back_substitute(cse_evaluator* ev, const double* d_x, double* d_y) {
+  int rc = SchurCheck(ev, true);
+  if (rc) return rc;
+  if (!d_x || !d_y) return Fail(CSE_ERR_INVALID, "null pointer");
+  const auto& S = ev->schur;
+  hipStream_t s = ev->stream;
+  // e part: (E^T E + D_e^2)^-1 E^T (b - F x); f part: x.
+  CSE_HIP(hipMemsetAsync(d_y, 0, S.e_cols * sizeof(double), s));
+  LaunchSchurPass<cse::kSchurBack>(MakeSchurArgs(ev, d_x, d_y), s);
+  CSE_HIP(hipGetLastError());
+  CSE_HIP(hipMemcpyAsync(d_y + S.e_cols, d_x, S.f_cols * sizeof(double), hipMemcpyDeviceToDevice, s));
   return CSE_OK;
 }
 

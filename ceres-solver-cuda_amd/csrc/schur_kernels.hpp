@@ -1,0 +1,491 @@
+// schur_kernels.hpp -- the implicit Schur complement on the evaluator's
+// BlockSparseMatrix: ITERATIVE_SCHUR's linear operator and preconditioners
+// (internal/ceres/implicit_schur_complement.cc, iterative_schur_complement_
+// solver.cc, schur_jacobi_preconditioner.cc), on the Jacobian values where the
+// evaluator wrote them in HBM.
+//
+// Structure (a Schur-ordered BAL problem): residual block i has one f block
+// (slot 0, the camera: an F cell of 2 x S0 at f_base + 2 S0 i) and one e
+// block (slot 1, the point: an E cell of 2 x 3 at e_base + 6 i); blocks are
+// sorted by e block, so each e block's rows are one contiguous run.  The
+// host cuts the runs into wave chunks of whole runs (at most 64 blocks);
+// runs longer than a wave are the "big" e blocks, one wave each.
+//
+// With M_p = (E_p^T E_p + D_p^2)^-1 (3 x 3 per e block) the Schur complement
+// is S = F^T F + D_f^2 - F^T E M E^T F.  Every operation below is, per e
+// block p and its rows b:
+//     s_p = sum_b E_b^T z_b,   w_p = M_p s_p,   u_b = z_b - E_b w_p
+// followed by the f-block sum y_c += sum_{b of c} F_b^T u_b (the blocks'
+// F_b^T u_b are written in block order and summed per f block in a fixed
+// order by GradientContribKernel + GradientChunkReduceKernel, as the fused
+// gradient's camera rows), with
+//     init (UpdateRhs, implicit_schur_complement.cc:240-273):  z_b = b_b,
+//          and M_p computed and stored (AddDiagonalAndInvert, :190-214)
+//     multiply (RightMultiplyAndAccumulate, :101-141):  z_b = F_b x_c
+//     back substitution (BackSubstitute, :216-238):  z_b = b_b - F_b x_c,
+//          y_p = w_p, no f-block sum.
+// All sums run in a fixed order: results are bit-identical run to run.
+#ifndef CSE_SCHUR_KERNELS_HPP_
+#define CSE_SCHUR_KERNELS_HPP_
+
+#include "operator_kernels.hpp"
+
+namespace cse {
+
+enum SchurMode { kSchurInit = 0, kSchurMultiply = 1, kSchurBack = 2 };
+
+struct SchurArgs {
+  int64_t n;               // residual blocks
+  const int32_t* ids;      // [n][2]: f block (slot 0), e block (slot 1)
+  const double* jac;       // BlockSparseMatrix values
+  int64_t f_base, e_base;  // cell of block i: F at f_base + 2 S0 i, E at e_base + 6 i
+  int64_t f_col_base;      // f-vector index of f block id: f_col_base + S0 id
+  int64_t e_col_base;      // e column of e block id: e_col_base + 3 id
+  int64_t e_cols;          // D[e_cols + k] scales f column k
+  const double* D;         // [e_cols + f_cols], may be null
+  const double* b;         // right-hand side rows: block i's pair at b + b_base + 2 i
+  int64_t b_base;
+  const double* x;         // f vector (multiply, back substitution)
+  double* ete_inv;         // M_p, packed upper triangle, at ete_inv + 2 * (e column of p)
+  double* contrib;         // [n][S0p] F_b^T u_b
+  double* y;               // back substitution: the full solution (e part written)
+  const int64_t* chunk_begin;  // [nchunks][2] begin, end: wave chunks of whole e-block runs
+  int64_t nchunks;
+  const int64_t* big;      // [nbig][2] runs longer than a wave
+  int64_t nbig;
+};
+
+// Packed upper triangle of a symmetric 3 x 3: (00, 01, 02, 11, 12, 22).
+// M = (A + diag(d^2))^-1 by the Cholesky factor, as the reference's
+// m.selfadjointView<Upper>().llt().solve(Identity) (implicit_schur_
+// complement.cc:207-211): A = L L^T, M = L^-T L^-1.
+__device__ __forceinline__ void InvertSpd3(const double* A, const double* d, double* M) {
+  const double a00 = A[0] + d[0] * d[0], a11 = A[3] + d[1] * d[1], a22 = A[5] + d[2] * d[2];
+  const double l00 = sqrt(a00);
+  const double i00 = 1.0 / l00;
+  const double l10 = A[1] * i00, l20 = A[2] * i00;
+  const double l11 = sqrt(a11 - l10 * l10);
+  const double i11 = 1.0 / l11;
+  const double l21 = (A[4] - l20 * l10) * i11;
+  const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
+  const double i22 = 1.0 / l22;
+  // L^-1 (lower): rows (i00), (j10 i11), (j20 j21 i22).
+  const double j10 = -l10 * i00 * i11;
+  const double j21 = -l21 * i11 * i22;
+  const double j20 = -(l20 * i00 + l21 * j10) * i22;
+  M[0] = i00 * i00 + j10 * j10 + j20 * j20;
+  M[1] = j10 * i11 + j20 * j21;
+  M[2] = j20 * i22;
+  M[3] = i11 * i11 + j21 * j21;
+  M[4] = j21 * i22;
+  M[5] = i22 * i22;
+}
+
+__device__ __forceinline__ void SymMul3(const double* M, const double* s, double* w) {
+  w[0] = M[0] * s[0] + M[1] * s[1] + M[2] * s[2];
+  w[1] = M[1] * s[0] + M[3] * s[1] + M[4] * s[2];
+  w[2] = M[2] * s[0] + M[4] * s[1] + M[5] * s[2];
+}
+
+// One block's cells and z_b.
+template <int S0, int kMode>
+__device__ __forceinline__ void SchurLoadBlock(const SchurArgs& a, int64_t i, int id0, double* F,
+                                               double* E, double* z) {
+  const double2* ep = reinterpret_cast<const double2*>(a.jac + a.e_base + 6 * i);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double2 v = ep[k];
+    E[2 * k] = v.x;
+    E[2 * k + 1] = v.y;
+  }
+  {
+    const double2* fp = reinterpret_cast<const double2*>(a.jac + a.f_base + 2 * S0 * i);
+#pragma unroll
+    for (int k = 0; k < S0; ++k) {
+      const double2 v = fp[k];
+      F[2 * k] = v.x;
+      F[2 * k + 1] = v.y;
+    }
+  }
+  if constexpr (kMode != kSchurMultiply) {
+    const double2 v = *reinterpret_cast<const double2*>(a.b + a.b_base + 2 * i);
+    z[0] = v.x;
+    z[1] = v.y;
+  }
+  if constexpr (kMode != kSchurInit) {
+    const double* xc = a.x + a.f_col_base + (int64_t)S0 * id0;
+    double f0 = 0.0, f1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < S0; ++k) {
+      const double xv = xc[k];
+      f0 += F[k] * xv;
+      f1 += F[S0 + k] * xv;
+    }
+    if constexpr (kMode == kSchurMultiply) {
+      z[0] = f0;
+      z[1] = f1;
+    } else {
+      z[0] -= f0;
+      z[1] -= f1;
+    }
+  }
+}
+
+// E_b^T z (3) and, for init, E_b^T E_b (packed, 6).
+__device__ __forceinline__ void SchurEProducts(const double* E, const double* z, double* s,
+                                               double* A) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = E[k] * z[0] + E[3 + k] * z[1];
+  A[0] = E[0] * E[0] + E[3] * E[3];
+  A[1] = E[0] * E[1] + E[3] * E[4];
+  A[2] = E[0] * E[2] + E[3] * E[5];
+  A[3] = E[1] * E[1] + E[4] * E[4];
+  A[4] = E[1] * E[2] + E[4] * E[5];
+  A[5] = E[2] * E[2] + E[5] * E[5];
+}
+
+// u_b = z_b - E_b w, then F_b^T u_b (S0 values, padded to S0p) to contrib.
+template <int S0>
+__device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, const double* F,
+                                             const double* E, const double* z, const double* w) {
+  constexpr int S0p = (S0 + 1) & ~1;
+  const double u0 = z[0] - (E[0] * w[0] + E[1] * w[1] + E[2] * w[2]);
+  const double u1 = z[1] - (E[3] * w[0] + E[4] * w[1] + E[5] * w[2]);
+  double2* dst = reinterpret_cast<double2*>(a.contrib + (int64_t)S0p * i);
+#pragma unroll
+  for (int k = 0; k < S0p / 2; ++k) {
+    const double c0 = F[2 * k] * u0 + F[S0 + 2 * k] * u1;
+    const double c1 = 2 * k + 1 < S0 ? F[2 * k + 1] * u0 + F[S0 + 2 * k + 1] * u1 : 0.0;
+    dst[k] = make_double2(c0, c1);
+  }
+}
+
+// One wave per chunk of whole e-block runs.
+template <int S0, int kMode>
+__global__ __launch_bounds__(kBlockThreads) void SchurChunkKernel(const SchurArgs a) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (c >= a.nchunks) return;
+  const int64_t i0 = a.chunk_begin[2 * c];
+  const int nb = (int)(a.chunk_begin[2 * c + 1] - i0);
+  const bool active = lane < nb;
+  const int64_t i = active ? i0 + lane : i0;
+  const long long idw = reinterpret_cast<const long long*>(a.ids)[i];
+  const int id0 = (int)idw, id1 = (int)(idw >> 32);
+  double F[2 * S0], E[6], z[2];
+  SchurLoadBlock<S0, kMode>(a, i, id0, F, E, z);
+  double s[3], A[6];
+  SchurEProducts(E, z, s, A);
+  if (!active) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) A[k] = 0.0;
+  }
+  // Runs are whole inside the chunk: a segmented scan leaves each run's
+  // sums in its last lane, which every lane of the run then reads.
+  const int key = active ? id1 : -1;
+  SegmentedScan<3>(s, key, lane);
+  if constexpr (kMode == kSchurInit) SegmentedScan<6>(A, key, lane);
+  const int knext = __shfl_down(key, 1, kWave);
+  const bool is_end = lane == kWave - 1 || knext != key;
+  const uint64_t ends = __ballot(is_end);
+  const int e = (int)__builtin_ctzll(ends >> lane) + lane;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = __shfl(s[k], e, kWave);
+  const int64_t ecol = a.e_col_base + 3LL * id1;
+  double M[6];
+  if constexpr (kMode == kSchurInit) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) A[k] = __shfl(A[k], e, kWave);
+    double d[3] = {0.0, 0.0, 0.0};
+    if (a.D) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d[k] = a.D[ecol + k];
+    }
+    InvertSpd3(A, d, M);
+    if (active && lane == e) {
+      double* m = a.ete_inv + 2 * ecol;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) m[k] = M[k];
+    }
+  } else {
+    const double2* m = reinterpret_cast<const double2*>(a.ete_inv + 2 * ecol);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 v = m[k];
+      M[2 * k] = v.x;
+      M[2 * k + 1] = v.y;
+    }
+  }
+  double w[3];
+  SymMul3(M, s, w);
+  if (!active) return;
+  if constexpr (kMode == kSchurBack) {
+    if (lane == e) {
+      double* yp = a.y + ecol;
+      yp[0] = w[0];
+      yp[1] = w[1];
+      yp[2] = w[2];
+    }
+  } else {
+    SchurContrib<S0>(a, i, F, E, z, w);
+  }
+}
+
+// One wave per e block with more rows than a wave: the rows are walked
+// twice, once for the sums and once for the contributions.
+template <int S0, int kMode>
+__global__ __launch_bounds__(kBlockThreads) void SchurBigKernel(const SchurArgs a) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t q = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (q >= a.nbig) return;
+  const int64_t i0 = a.big[2 * q], i1 = a.big[2 * q + 1];
+  const int id1 = (int)(reinterpret_cast<const long long*>(a.ids)[i0] >> 32);
+  double s[3] = {0.0, 0.0, 0.0}, A[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = i0 + lane; i < i1; i += kWave) {
+    const int id0 = (int)reinterpret_cast<const long long*>(a.ids)[i];
+    double F[2 * S0], E[6], z[2], sb[3], Ab[6];
+    SchurLoadBlock<S0, kMode>(a, i, id0, F, E, z);
+    SchurEProducts(E, z, sb, Ab);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k] += sb[k];
+    if constexpr (kMode == kSchurInit) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] += Ab[k];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k] += __shfl_xor(s[k], off, kWave);
+    if constexpr (kMode == kSchurInit) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] += __shfl_xor(A[k], off, kWave);
+    }
+  }
+  const int64_t ecol = a.e_col_base + 3LL * id1;
+  double M[6];
+  if constexpr (kMode == kSchurInit) {
+    double d[3] = {0.0, 0.0, 0.0};
+    if (a.D) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d[k] = a.D[ecol + k];
+    }
+    InvertSpd3(A, d, M);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a.ete_inv[2 * ecol + k] = M[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) M[k] = a.ete_inv[2 * ecol + k];
+  }
+  double w[3];
+  SymMul3(M, s, w);
+  if constexpr (kMode == kSchurBack) {
+    if (lane == 0) {
+      a.y[ecol] = w[0];
+      a.y[ecol + 1] = w[1];
+      a.y[ecol + 2] = w[2];
+    }
+  } else {
+    for (int64_t i = i0 + lane; i < i1; i += kWave) {
+      const int id0 = (int)reinterpret_cast<const long long*>(a.ids)[i];
+      double F[2 * S0], E[6], z[2];
+      SchurLoadBlock<S0, kMode>(a, i, id0, F, E, z);
+      SchurContrib<S0>(a, i, F, E, z, w);
+    }
+  }
+}
+
+// y[k] = D[off + k]^2 x[k] (the D^2 x term of RightMultiplyAndAccumulate,
+// assigned: the reference sets y before adding F^T y1), or 0 without D.
+__global__ __launch_bounds__(kBlockThreads) void SchurDiagKernel(const double* D, int64_t off,
+                                                                 const double* x, double* y,
+                                                                 int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (k >= n) return;
+  if (D) {
+    const double d = D[off + k];
+    y[k] = d * d * x[k];
+  } else {
+    y[k] = 0.0;
+  }
+}
+
+// y += x.
+__global__ __launch_bounds__(kBlockThreads) void AxpyKernel(const double* x, double* y, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (k < n) y[k] += x[k];
+}
+
+// Block diagonal preconditioners over the f blocks, per block list chunk
+// (the camera plan of the gradient: chunks of at most kGradChunk rows of one
+// f block), one wave per chunk, each lane summing the packed upper
+// triangle of F_b^T Q_b F_b over its rows:
+//   JACOBI        Q_b = I: (F^T F + D_f^2)^-1, ImplicitSchurComplement's
+//                 block_diagonal_FtF_inverse (implicit_schur_complement.cc:
+//                 71-95, iterative_schur_complement_solver.cc:186-189);
+//   SCHUR_JACOBI  Q_b = I - E_b M_p E_b^T: the f-block diagonal of S
+//                 (schur_jacobi_preconditioner.cc:89-98; exact when no e
+//                 block sees one f block twice, which the host checks).
+template <int S0>
+constexpr int SymCount() { return S0 * (S0 + 1) / 2; }
+
+template <int S0, bool kSchur>
+__global__ __launch_bounds__(kBlockThreads) void SchurBlockDiagKernel(const SchurArgs a,
+                                                                      const int32_t* perm,
+                                                                      const GradChunks ch) {
+  constexpr int T = SymCount<S0>();
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (cid >= ch.nchunks) return;
+  double acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = 0.0;
+  const int64_t q1 = ch.begin[cid + 1];
+  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
+    const int64_t i = perm[q];
+    double F[2 * S0];
+    const double2* fp = reinterpret_cast<const double2*>(a.jac + a.f_base + 2 * S0 * i);
+#pragma unroll
+    for (int k = 0; k < S0; ++k) {
+      const double2 v = fp[k];
+      F[2 * k] = v.x;
+      F[2 * k + 1] = v.y;
+    }
+    double q00 = 1.0, q01 = 0.0, q11 = 1.0;
+    if constexpr (kSchur) {
+      const int id1 = (int)(reinterpret_cast<const long long*>(a.ids)[i] >> 32);
+      const double* m = a.ete_inv + 2 * (a.e_col_base + 3LL * id1);
+      double M[6], E[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) M[k] = m[k];
+      const double* ep = a.jac + a.e_base + 6 * i;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) E[k] = ep[k];
+      double me0[3], me1[3];
+      SymMul3(M, E, me0);
+      SymMul3(M, E + 3, me1);
+      q00 = 1.0 - (E[0] * me0[0] + E[1] * me0[1] + E[2] * me0[2]);
+      q01 = -(E[0] * me1[0] + E[1] * me1[1] + E[2] * me1[2]);
+      q11 = 1.0 - (E[3] * me1[0] + E[4] * me1[1] + E[5] * me1[2]);
+    }
+    // F^T Q F, upper triangle row by row.
+    double g0[S0], g1[S0];  // Q F columns: rows 0 and 1
+#pragma unroll
+    for (int k = 0; k < S0; ++k) {
+      g0[k] = q00 * F[k] + q01 * F[S0 + k];
+      g1[k] = q01 * F[k] + q11 * F[S0 + k];
+    }
+    int t = 0;
+#pragma unroll
+    for (int r = 0; r < S0; ++r)
+#pragma unroll
+      for (int cc = r; cc < S0; ++cc) acc[t++] += F[r] * g0[cc] + F[S0 + r] * g1[cc];
+  }
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[t] += __shfl_xor(acc[t], off, kWave);
+  if (lane == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) ch.partial[cid * T + t] = acc[t];
+  }
+}
+
+// Per f block: its chunk partials summed in order, D^2 on the diagonal, the
+// inverse by the Cholesky factor (llt().solve(Identity), as the
+// reference's BlockRandomAccessDiagonalMatrix::Invert and AddDiagonalAndInvert)
+// stored as a full S0 x S0 matrix.
+template <int S0>
+__global__ __launch_bounds__(64) void SchurBlockInvertKernel(const GradChunks ch, int64_t count,
+                                                             const double* D, int64_t d_off,
+                                                             double* P) {
+  constexpr int T = SymCount<S0>();
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= count) return;
+  double L[S0][S0];
+  {
+    double acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = 0.0;
+    for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q)
+#pragma unroll
+      for (int t = 0; t < T; ++t) acc[t] += ch.partial[q * T + t];
+    int t = 0;
+#pragma unroll
+    for (int r = 0; r < S0; ++r)
+#pragma unroll
+      for (int cc = r; cc < S0; ++cc) L[cc][r] = acc[t++];  // lower triangle of A
+  }
+  if (D) {
+#pragma unroll
+    for (int r = 0; r < S0; ++r) {
+      const double d = D[d_off + (int64_t)S0 * p + r];
+      L[r][r] += d * d;
+    }
+  }
+  // In-place Cholesky: A = L L^T.
+#pragma unroll
+  for (int j = 0; j < S0; ++j) {
+    double djj = L[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) djj -= L[j][k] * L[j][k];
+    const double ljj = sqrt(djj);
+    const double inv = 1.0 / ljj;
+    L[j][j] = ljj;
+#pragma unroll
+    for (int r = j + 1; r < S0; ++r) {
+      double v = L[r][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) v -= L[r][k] * L[j][k];
+      L[r][j] = v * inv;
+    }
+  }
+  // Columns of the inverse: L y = e_c, then L^T x = y.
+  double* out = P + (int64_t)S0 * S0 * p;
+#pragma unroll
+  for (int cc = 0; cc < S0; ++cc) {
+    double y[S0];
+#pragma unroll
+    for (int r = 0; r < S0; ++r) {
+      double v = r == cc ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < r; ++k) v -= L[r][k] * y[k];
+      y[r] = v / L[r][r];
+    }
+#pragma unroll
+    for (int r = S0 - 1; r >= 0; --r) {
+      double v = y[r];
+#pragma unroll
+      for (int k = r + 1; k < S0; ++k) v -= L[k][r] * y[k];
+      y[r] = v / L[r][r];
+    }
+#pragma unroll
+    for (int r = 0; r < S0; ++r) out[r * S0 + cc] = y[r];
+  }
+}
+
+// y += P x per f block (the preconditioner's RightMultiplyAndAccumulate),
+// one thread per f-vector entry.
+template <int S0>
+__global__ __launch_bounds__(kBlockThreads) void SchurPrecondApplyKernel(const double* P,
+                                                                         const double* x,
+                                                                         double* y, int64_t n) {
+  const int64_t k = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (k >= n) return;
+  const int64_t p = k / S0;
+  const int r = (int)(k - p * S0);
+  const double* row = P + (int64_t)S0 * S0 * p + (int64_t)S0 * r;
+  const double* xp = x + (int64_t)S0 * p;
+  double v = 0.0;
+#pragma unroll
+  for (int cc = 0; cc < S0; ++cc) v += row[cc] * xp[cc];
+  y[k] += v;
+}
+
+}  // namespace cse
+
+#endif  // CSE_SCHUR_KERNELS_HPP_

@@ -255,6 +255,51 @@ int cse_jacobian_left_multiply(cse_evaluator* ev, const double* d_jacobian_value
 int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
                       const double* d_x, double* d_y);
 
+/* ---- ITERATIVE_SCHUR on the device -------------------------------------
+ * The implicit Schur complement of the Jacobian this evaluator wrote, for
+ * the linear solve of a Schur-ordered bundle adjustment problem: replaces
+ * ImplicitSchurComplement (internal/ceres/implicit_schur_complement.h:
+ * 86-160) and the preconditioners IterativeSchurComplementSolver builds
+ * (iterative_schur_complement_solver.cc:172-204).  With the Jacobian
+ * A = [E F] (e blocks = the points, slot 1; f blocks = the cameras, slot 0),
+ * a per-column diagonal D and the right-hand side b, the system
+ * (A^T A + D^2) [y_e; y_f] = A^T b is reduced to
+ *     S y_f = rhs,  S = F^T F + D_f^2 - F^T E (E^T E + D_e^2)^-1 E^T F,
+ *     rhs = F^T (b - E (E^T E + D_e^2)^-1 E^T b).
+ * Requires (CSE_ERR_UNSUPPORTED otherwise) one Snavely group on the affine
+ * BlockSparseMatrix path whose points occupy the effective columns
+ * [0, num_cols_e) and cameras the rest, as ITERATIVE_SCHUR's elimination
+ * ordering gives.  All device pointers, asynchronous on the evaluator's
+ * stream, deterministic. */
+enum cse_schur_preconditioner {
+  CSE_SCHUR_IDENTITY = 0,     /* IDENTITY: M^-1 = I */
+  CSE_SCHUR_JACOBI = 1,       /* JACOBI: block diagonal (F^T F + D_f^2)^-1 */
+  CSE_SCHUR_SCHUR_JACOBI = 2  /* SCHUR_JACOBI: block diagonal of S, inverted
+                                 (schur_jacobi_preconditioner.cc:89-98) */
+};
+
+/* The column split: num_cols_e (points) and num_cols_f (cameras). */
+int cse_schur_structure(cse_evaluator* ev, int64_t* num_cols_e, int64_t* num_cols_f);
+
+/* ImplicitSchurComplement::Init(A, D, b) (implicit_schur_complement.cc:
+ * 53-99) plus Preconditioner::Update: binds d_jacobian_values, d_D
+ * (num_effective_parameters entries, may be NULL) and d_b (num_residuals)
+ * -- they must stay valid until the next init -- computes the per-point
+ * (E^T E + D_e^2)^-1, writes rhs (num_cols_f) and builds the preconditioner. */
+int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                   const double* d_b, double* d_rhs, int preconditioner);
+
+/* y = S x (ImplicitSchurComplement::RightMultiplyAndAccumulate, :101-141,
+ * which assigns y); x and y have num_cols_f entries. */
+int cse_schur_multiply(cse_evaluator* ev, const double* d_x, double* d_y);
+
+/* y += M^-1 x for the preconditioner chosen at init. */
+int cse_schur_precondition(cse_evaluator* ev, const double* d_x, double* d_y);
+
+/* ImplicitSchurComplement::BackSubstitute(x, y) (:216-238): y
+ * (num_effective_parameters) = [(E^T E + D_e^2)^-1 E^T (b - F x); x]. */
+int cse_schur_back_substitute(cse_evaluator* ev, const double* d_x, double* d_y);
+
 void cse_destroy(cse_evaluator* ev);
 
 /* Thread-local description of the last error. */
