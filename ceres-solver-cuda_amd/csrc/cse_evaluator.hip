@@ -266,6 +266,10 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 5: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, false>, 4>;
     case 6: return &LaunchBounded<K, L, true, false, 2, cse::Tune<1, false>, 4>;
     case 7: return &LaunchBounded<K, L, true, false, 2, cse::Tune<2, false>, 4>;
+    case 12: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, true>>;
+    case 13: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true>, 4>;
+    case 14: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, true, 28>>;
+    case 15: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 28>>;
     default: return nullptr;
   }
 }

@@ -333,10 +333,16 @@ __device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw)
 //   kLdsE   stage the slot-1 (E) cells through LDS with the F cells (true),
 //           or store each lane's E cell straight from registers, 48 B per
 //           lane (false: 2/3 of the LDS, 4 workgroups per CU).
-template <int kPrio_ = 0, bool kLdsE_ = true>
+//   kTwoRound  stage the F cells, read them back, then stage the E cells in
+//           the same LDS (9 KiB a wave instead of 12: 4 workgroups per CU).
+//   kMinLane  at least this many doubles of LDS per lane (an occupancy
+//           limit: 28 -> 56 KiB a workgroup, 2 workgroups per CU).
+template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
+  static constexpr bool kTwoRound = kTwoRound_;
+  static constexpr int kMinLane = kMinLane_;
 };
 // Shipped: no priority changes.  kPrio 2 was 1.5-2 % faster with the
 // library sincos and divisions (profiles/round2/s1, s3c) and 2 % slower
@@ -359,13 +365,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = S0 + S1;
   static_assert(!MayLeaveOutputs<K>::value, "affine kernels: functors that assign every output");
   constexpr bool kLdsE = T::kLdsE || kCrs || !kJac;
-  constexpr int kOutLane = kJac ? (kCrs ? NR * N : kLdsE ? NR * (S0 + S1) : NR * S0) : 1;
+  constexpr bool kTwo = T::kTwoRound && kJac && !kCrs && kLdsE && S1 > 0;
+  constexpr int kOutLane = kJac ? (kCrs ? NR * N
+                                        : kTwo ? NR * (S0 > S1 ? S0 : S1)
+                                               : kLdsE ? NR * (S0 + S1) : NR * S0)
+                                : 1;
   constexpr int kCoopLane = kCoop == 2 ? ((S0 + 1) & ~1) : S0;
   // StageAndStore's footprint (ragged chunks): whole rows (CRS) or one
   // slot's cells at a time (BSM).
   constexpr int kSlowLane = !kJac ? 1 : kCrs ? NR * N : NR * (S0 > S1 ? S0 : S1);
   constexpr int kStageLane0 = kCoopLane > kOutLane ? kCoopLane : kOutLane;
-  constexpr int kStageLane = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
+  constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
+  constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
   __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -487,7 +498,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 #pragma unroll
         for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
         if constexpr (S1 > 0) {
-          if constexpr (kLdsE) {
+          if constexpr (kLdsE && !kTwo) {
 #pragma unroll
             for (int k = 0; k < NR; ++k)
 #pragma unroll
@@ -504,7 +515,21 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         q0[j] = AsV4i(v.x, v.y);
       }
       if constexpr (kQ1 > 0) {
-        if constexpr (kLdsE) {
+        if constexpr (kTwo) {
+          // Second round: the E cells in the LDS the F pieces came from.
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int j = 0; j < kQ1; ++j) {
+            const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
+            q1[j] = AsV4i(v.x, v.y);
+          }
+        } else if constexpr (kLdsE) {
           const double* st1 = st + kWave * NR * S0;
 #pragma unroll
           for (int j = 0; j < kQ1; ++j) {

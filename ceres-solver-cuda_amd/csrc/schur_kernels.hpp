@@ -160,20 +160,81 @@ __device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, cons
   }
 }
 
-// One wave per chunk of whole e-block runs.
+// One wave per chunk of whole e-block runs.  The chunk's F cells and E cells
+// are contiguous in the BlockSparseMatrix and come in by LDS-DMA (16-byte
+// pieces, up to 1 KiB per instruction), as CgnrMultiplyKernel's image; each
+// lane reads its block's cells from LDS.  The contributions F_b^T u_b are
+// staged through the same LDS and leave as contiguous 16-byte pieces.
 template <int S0, int kMode>
 __global__ __launch_bounds__(kBlockThreads) void SchurChunkKernel(const SchurArgs a) {
+  constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kF = 2 * S0;                // doubles per F cell
+  constexpr int kImg = kWave * (kF + 6);    // F cells, then E cells, of up to a wave of blocks
+  static_assert(kF % 2 == 0 && kWave * S0p <= kImg, "16-byte pieces; contributions fit");
+  __shared__ double img_all[kWavesPerBlock][kImg];
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (c >= a.nchunks) return;
+  double* im = img_all[wave];
   const int64_t i0 = a.chunk_begin[2 * c];
   const int nb = (int)(a.chunk_begin[2 * c + 1] - i0);
   const bool active = lane < nb;
   const int64_t i = active ? i0 + lane : i0;
+  {
+    const double* segF = a.jac + a.f_base + (int64_t)kF * i0;
+    const double* segE = a.jac + a.e_base + 6LL * i0;
+    const int pf = (kF / 2) * nb, pe = 3 * nb;  // 16-byte pieces
+#pragma unroll
+    for (int k = 0; k < kF / 2; ++k) {
+      const int p = k * kWave + lane;
+      if (p < pf) __builtin_amdgcn_global_load_lds(segF + 2 * p, im + 2 * kWave * k, 16, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int p = k * kWave + lane;
+      if (p < pe)
+        __builtin_amdgcn_global_load_lds(segE + 2 * p, im + kWave * kF + 2 * kWave * k, 16, 0, 0);
+    }
+  }
   const long long idw = reinterpret_cast<const long long*>(a.ids)[i];
   const int id0 = (int)idw, id1 = (int)(idw >> 32);
-  double F[2 * S0], E[6], z[2];
-  SchurLoadBlock<S0, kMode>(a, i, id0, F, E, z);
+  double z[2] = {0.0, 0.0};
+  if constexpr (kMode != kSchurMultiply) {
+    const double2 v = *reinterpret_cast<const double2*>(a.b + a.b_base + 2 * i);
+    z[0] = v.x;
+    z[1] = v.y;
+  }
+  double xc[S0];
+  if constexpr (kMode != kSchurInit) {
+    const double* xp = a.x + a.f_col_base + (int64_t)S0 * id0;
+#pragma unroll
+    for (int k = 0; k < S0; ++k) xc[k] = xp[k];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  double F[kF], E[6];
+#pragma unroll
+  for (int k = 0; k < kF / 2; ++k) {
+    const double2 v = reinterpret_cast<const double2*>(im + kF * lane)[k];
+    F[2 * k] = v.x;
+    F[2 * k + 1] = v.y;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double2 v = reinterpret_cast<const double2*>(im + kWave * kF + 6 * lane)[k];
+    E[2 * k] = v.x;
+    E[2 * k + 1] = v.y;
+  }
+  if constexpr (kMode != kSchurInit) {
+    double f0 = 0.0, f1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < S0; ++k) {
+      f0 += F[k] * xc[k];
+      f1 += F[S0 + k] * xc[k];
+    }
+    z[0] = kMode == kSchurMultiply ? f0 : z[0] - f0;
+    z[1] = kMode == kSchurMultiply ? f1 : z[1] - f1;
+  }
   double s[3], A[6];
   SchurEProducts(E, z, s, A);
   if (!active) {
@@ -220,16 +281,34 @@ __global__ __launch_bounds__(kBlockThreads) void SchurChunkKernel(const SchurArg
   }
   double w[3];
   SymMul3(M, s, w);
-  if (!active) return;
   if constexpr (kMode == kSchurBack) {
-    if (lane == e) {
+    if (active && lane == e) {
       double* yp = a.y + ecol;
       yp[0] = w[0];
       yp[1] = w[1];
       yp[2] = w[2];
     }
   } else {
-    SchurContrib<S0>(a, i, F, E, z, w);
+    // F_b^T u_b, staged over the consumed image, out as contiguous pieces.
+    const double u0 = z[0] - (E[0] * w[0] + E[1] * w[1] + E[2] * w[2]);
+    const double u1 = z[1] - (E[3] * w[0] + E[4] * w[1] + E[5] * w[2]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < S0p / 2; ++k) {
+      const double c0 = F[2 * k] * u0 + F[S0 + 2 * k] * u1;
+      const double c1 = 2 * k + 1 < S0 ? F[2 * k + 1] * u0 + F[S0 + 2 * k + 1] * u1 : 0.0;
+      reinterpret_cast<double2*>(im + S0p * lane)[k] = make_double2(c0, c1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    v2d* dst = reinterpret_cast<v2d*>(a.contrib + (int64_t)S0p * i0);
+    const int pc = (S0p / 2) * nb;
+#pragma unroll
+    for (int k = 0; k < S0p / 2; ++k) {
+      const int p = k * kWave + lane;
+      if (p < pc) __builtin_nontemporal_store(reinterpret_cast<const v2d*>(im)[p], dst + p);
+    }
   }
 }
 

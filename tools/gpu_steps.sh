@@ -30,6 +30,11 @@ for s in "$@"; do
     bench2) timeout -k 10 600 python -u bench.py --gpus 2 --steps 10 --no-cpu-baseline \
               > "$OUT/bench2.json" 2> "$OUT/bench2.err"; rc=$?
             tail -c 2500 "$OUT/bench2.json"; tail -5 "$OUT/bench2.err" ;;
+    bm:*)   # bm:MODE -- bench.py --mode MODE (no CPU baseline, no secondary legs)
+            m=${s#bm:}
+            timeout -k 10 300 python -u bench.py --mode $m --no-cpu-baseline --no-secondary --steps 20 \
+              > "$OUT/bench_$m.json" 2> "$OUT/bench_$m.err"; rc=$?
+            python3 -c "import json,sys; b=json.loads(open('$OUT/bench_$m.json').read().strip().splitlines()[-1]); print('$m', round(b['ms_per_step'],4), 'ms', round(b['roofline']['frac'],4))" ;;
     prof)   mkdir -p "$OUT/prof"
             timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
               --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 10 \
