@@ -88,6 +88,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the box's CPU share ($OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="single process: evaluate only rank 0's shard of an N-way point-bucket "
+                         "cut (the per-rank work of an N-GPU strong-scaling run, without the "
+                         "collectives); reported with value = shard evaluations/s, not the headline")
     return ap.parse_args()
 
 
@@ -252,6 +256,10 @@ def main():
     counts = bal.CONFIGS[args.config]
     arrays = bal.synthetic(*counts, seed=args.seed + (0 if strong else rank))
     srank, sworld = (rank, world) if strong else (0, 1)
+    if args.shard_of > 1:
+        if world != 1:
+            raise SystemExit("--shard-of is a single-process measurement")
+        srank, sworld = 0, args.shard_of
     stream = torch.cuda.current_stream(dev)
     se = distributed.ShardedEvaluator(*arrays, srank, sworld, device=dev_index,
                                       loss=make_loss(args.loss), format=args.format,
@@ -446,7 +454,8 @@ def main():
                             + f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
                 "blocks_rank0": sh.blocks[1] - sh.blocks[0],
-                "parallelism": ("single GPU" if world == 1 else
+                "parallelism": (f"rank 0's shard of {args.shard_of} (one process)" if args.shard_of > 1
+                                else "single GPU" if world == 1 else
                                 f"point-bucket block sharding x{world}" if strong else
                                 f"replica shards x{world}"),
                 "exchange": (None if world == 1 else

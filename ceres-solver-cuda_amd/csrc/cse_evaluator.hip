@@ -270,6 +270,7 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 13: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true>, 4>;
     case 14: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, true, 28>>;
     case 15: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 28>>;
+    case 16: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 128>>;
     default: return nullptr;
   }
 }

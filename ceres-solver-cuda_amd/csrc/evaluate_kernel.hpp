@@ -324,6 +324,46 @@ __device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw)
   return (m & 15) == 0;
 }
 
+// Sector-aligned store windows.  A wave's output segment of kQ wave
+// instructions (kQ * 64 pieces of 16 bytes) starts at some byte S; when S is
+// not on a 64-byte HBM sector boundary (the BlockSparseMatrix F cells start
+// at 6 * num_blocks doubles, so this depends on the block count), every 1 KiB
+// store instruction would begin and end inside a sector, and each of its two
+// partial sectors leaves the streaming L2 path as a separate masked write:
+// the kernel then ran at 0.45 instead of 0.60-0.65 of 8 TB/s
+// (profiles/round2/s3n/fracs.txt: bimodal in block count mod 4).  So the
+// pieces are regrouped: the first hp pieces (hp = pieces to the next sector
+// boundary, 0..3) and the last 4 - hp are the segment's partial sectors,
+// stored by lanes 60..63 of the last instruction; every other instruction
+// writes 1 KiB of whole sectors, starting hp pieces into the segment.  With
+// hp = 0 this is the plain in-order tiling.
+// kA: the alignment unit in bytes (64: an HBM sector; 128: an L2 line).
+template <int kA = 64>
+__device__ __forceinline__ int SectorHeadPieces(const double* seg) {
+  constexpr uint32_t m = kA - 1;
+  return (int)(((kA - ((uint32_t)reinterpret_cast<uintptr_t>(seg) & m)) & m) >> 4);
+}
+// Piece of the segment that `lane` stores in the last instruction.
+template <int kQ, int kA = 64>
+__device__ __forceinline__ int LastPiece(int lane, int hp) {
+  constexpr int kEdge = kA / 16;  // lanes carrying the head and tail pieces
+  const int k = lane - (kWave - kEdge);
+  return k < 0 ? (kQ - 1) * kWave + lane + hp : (k < hp ? k : kQ * kWave - kEdge + k);
+}
+// The kQ pieces this lane stores, read back from the wave's staged segment.
+template <int kQ, int kA = 64>
+__device__ __forceinline__ void ReadSegmentPieces(const double* staged, int hp, int lane,
+                                                  cse_v4i* q) {
+  const double2* st2 = reinterpret_cast<const double2*>(staged);
+#pragma unroll
+  for (int j = 0; j < kQ - 1; ++j) {
+    const double2 v = st2[j * kWave + lane + hp];
+    q[j] = AsV4i(v.x, v.y);
+  }
+  const double2 v = st2[LastPiece<kQ, kA>(lane, hp)];
+  q[kQ - 1] = AsV4i(v.x, v.y);
+}
+
 // Compile-time knobs of the affine kernel.  The product instantiates only
 // ShippedTune; other settings exist in the tuning build (-DCSE_TUNING,
 // tools/), never in libcse.so.
@@ -337,12 +377,15 @@ __device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw)
 //           the same LDS (9 KiB a wave instead of 12: 4 workgroups per CU).
 //   kMinLane  at least this many doubles of LDS per lane (an occupancy
 //           limit: 28 -> 56 KiB a workgroup, 2 workgroups per CU).
-template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0>
+//   kAlign  the store windows' alignment unit (SectorHeadPieces), bytes.
+template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
+          int kAlign_ = 64>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
   static constexpr bool kTwoRound = kTwoRound_;
   static constexpr int kMinLane = kMinLane_;
+  static constexpr int kAlign = kAlign_;
 };
 // Shipped: no priority changes.  kPrio 2 was 1.5-2 % faster with the
 // library sincos and divisions (profiles/round2/s1, s3c) and 2 % slower
@@ -366,6 +409,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   static_assert(!MayLeaveOutputs<K>::value, "affine kernels: functors that assign every output");
   constexpr bool kLdsE = T::kLdsE || kCrs || !kJac;
   constexpr bool kTwo = T::kTwoRound && kJac && !kCrs && kLdsE && S1 > 0;
+  constexpr int kA = T::kAlign;
   constexpr int kOutLane = kJac ? (kCrs ? NR * N
                                         : kTwo ? NR * (S0 > S1 ? S0 : S1)
                                                : kLdsE ? NR * (S0 + S1) : NR * S0)
@@ -475,6 +519,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   cse_v4i q0[kQ0 > 0 ? kQ0 : 1], q1[kQ1 > 0 ? kQ1 : 1];
   double* seg0 = nullptr;
   double* seg1 = nullptr;
+  int hp0 = 0, hp1 = 0;  // pieces to the first sector boundary (SectorHeadPieces)
   if constexpr (kJac) {
     if (jac) {
       if constexpr (kCrs) {
@@ -509,12 +554,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
       }
       __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int j = 0; j < kQ0; ++j) {
-        const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
-        q0[j] = AsV4i(v.x, v.y);
-      }
+      hp0 = SectorHeadPieces<kA>(seg0);
+      ReadSegmentPieces<kQ0, kA>(st, hp0, lane, q0);
       if constexpr (kQ1 > 0) {
+        hp1 = SectorHeadPieces<kA>(seg1);
         if constexpr (kTwo) {
           // Second round: the E cells in the LDS the F pieces came from.
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -524,18 +567,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 #pragma unroll
             for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
           __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int j = 0; j < kQ1; ++j) {
-            const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
-            q1[j] = AsV4i(v.x, v.y);
-          }
+          ReadSegmentPieces<kQ1, kA>(st, hp1, lane, q1);
         } else if constexpr (kLdsE) {
-          const double* st1 = st + kWave * NR * S0;
-#pragma unroll
-          for (int j = 0; j < kQ1; ++j) {
-            const double2 v = reinterpret_cast<const double2*>(st1)[j * kWave + lane];
-            q1[j] = AsV4i(v.x, v.y);
-          }
+          ReadSegmentPieces<kQ1, kA>(st + kWave * NR * S0, hp1, lane, q1);
         } else {
           // The lane's own cell, row-major (NR x S1, S1p == S1 here).
 #pragma unroll
@@ -579,16 +613,20 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   // the empty asm) before the first store: after it the wave runs only
   // stores and SALU, so nothing waits on the store queue.
   double *f0 = nullptr, *f1 = nullptr, *e0 = nullptr, *e1 = nullptr;
+  double *flast = nullptr, *elast = nullptr;
   if (jac) {
-    f0 = seg0 + 2 * lane + 512;
-    f1 = seg0 + 2 * lane + 1536;
+    f0 = seg0 + 2 * (lane + hp0) + 512;
+    f1 = seg0 + 2 * (lane + hp0) + 1536;
+    flast = seg0 + 2 * LastPiece<(kQ0 > 0 ? kQ0 : 1), kA>(lane, hp0);
     if constexpr (kQ1 > 0) {
       if constexpr (kLdsE) {
-        e0 = seg1 + 2 * lane + 512;
-        e1 = seg1 + 2 * lane + 1536;
+        e0 = seg1 + 2 * (lane + hp1) + 512;
+        e1 = seg1 + 2 * (lane + hp1) + 1536;
+        elast = seg1 + 2 * LastPiece<kQ1, kA>(lane, hp1);
       } else {
         e0 = seg1 + NR * S1 * lane;  // the lane's own 48-byte cell
         e1 = e0;
+        elast = e0;
       }
     }
   }
@@ -596,14 +634,16 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   double* v_partial = partial_dst;
   double v_wsum = wsum;
   asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
-  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst));
+  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(flast), "v"(elast));
 
   // ---- every store of the wave, back to back ----
   if (jac) {
-    SegmentStoresFrom<0, kQ0>(f0, f1, q0);
+    SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0)>(f0, f1, q0);
+    if constexpr (kQ0 > 0) StoreNt16<0>(flast, q0[kQ0 - 1]);
     if constexpr (kQ1 > 0) {
       if constexpr (kLdsE) {
-        SegmentStoresFrom<0, kQ1>(e0, e1, q1);
+        SegmentStoresFrom<0, kQ1 - 1>(e0, e1, q1);
+        StoreNt16<0>(elast, q1[kQ1 - 1]);
       } else {
         // Per-lane pieces at a 48-byte lane stride: each instruction covers
         // a third of every line of the segment, default policy so that the
@@ -640,7 +680,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
   KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
   KeepAlive<kQr>(qr);
-  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(v_partial), "v"(v_wsum));
+  asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(v_partial), "v"(v_wsum),
+               "v"(flast), "v"(elast));
   if constexpr (kGradF) {
     KeepAlive<kGQ>(gq);
     KeepAlive<2>(sq);

@@ -35,6 +35,11 @@ for s in "$@"; do
             timeout -k 10 300 python -u bench.py --mode $m --no-cpu-baseline --no-secondary --steps 20 \
               > "$OUT/bench_$m.json" 2> "$OUT/bench_$m.err"; rc=$?
             python3 -c "import json,sys; b=json.loads(open('$OUT/bench_$m.json').read().strip().splitlines()[-1]); print('$m', round(b['ms_per_step'],4), 'ms', round(b['roofline']['frac'],4))" ;;
+    shard:*) # shard:N -- bench.py --shard-of N (rank 0's per-GPU work of an N-way run)
+            m=${s#shard:}
+            timeout -k 10 300 python -u bench.py --shard-of $m --no-cpu-baseline --no-secondary --steps 50 \
+              > "$OUT/bench_shard$m.json" 2> "$OUT/bench_shard$m.err"; rc=$?
+            python3 -c "import json,sys; b=json.loads(open('$OUT/bench_shard$m.json').read().strip().splitlines()[-1]); print('shard of $m', round(b['ms_per_step'],4), 'ms/step', round(b['roofline']['kernel_ms_avg'],4), 'ms kernel', round(b['roofline']['frac'],4))" ;;
     prof)   mkdir -p "$OUT/prof"
             timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
               --output-format csv -- python3 bench.py --no-cpu-baseline --no-secondary --steps 10 \
