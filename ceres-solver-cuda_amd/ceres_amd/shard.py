@@ -24,10 +24,18 @@ from . import bal
 from .problem import BLOCK_SPARSE, COMPRESSED_ROW
 
 
-def point_bucket_cuts(pt_idx, num_points, world):
+def point_bucket_cuts(pt_idx, num_points, world, align=4, search=64):
     """Block ranges per rank, cut at point-bucket boundaries.  pt_idx must be
     point-major (nondecreasing).  Returns (point_cuts, block_cuts), each of
-    length world + 1."""
+    length world + 1.
+
+    Each cut is moved to the first point boundary at or after its target
+    whose block index is a multiple of `align` (looking at most `search`
+    boundaries ahead; else the plain boundary).  With align = 4 every
+    rank's block count is a multiple of 4, so its rank-local
+    BlockSparseMatrix F cells (at 6 * blocks doubles) start on a 64-byte
+    sector and the evaluator's store windows need no partial sectors
+    (DESIGN.md §4.3)."""
     pt_idx = np.asarray(pt_idx)
     if pt_idx.size and np.any(np.diff(pt_idx) < 0):
         raise ValueError("observations must be point-major (Schur order)")
@@ -38,6 +46,11 @@ def point_bucket_cuts(pt_idx, num_points, world):
     for r in range(1, world):
         target = O * r // world
         p = int(np.searchsorted(csum, target))  # first point whose start >= target
+        if align > 1:
+            window = csum[p:p + search]
+            hit = np.nonzero(window % align == 0)[0]
+            if hit.size:
+                p += int(hit[0])
         pc.append(max(p, pc[-1]))
     pc.append(int(num_points))
     bc = [int(csum[p]) for p in pc]

@@ -109,3 +109,10 @@ def test_point_bucket_cuts_properties():
                 assert pt[bc[r] - 1] < pt[bc[r]]
     with pytest.raises(ValueError):
         shard.point_bucket_cuts(pt[::-1], 1000, 2)
+    # Cuts land on block indices that are multiples of 4 (sector-aligned
+    # rank-local F cells) and stay close to the balanced target.
+    for world in (2, 3, 8):
+        pc, bc = shard.point_bucket_cuts(pt, 1000, world)
+        assert all(b % 4 == 0 for b in bc[1:-1])
+        for r in range(1, world):
+            assert abs(bc[r] - len(pt) * r // world) <= 64 * 40
