@@ -88,6 +88,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the box's CPU share ($OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: order each cost all-reduce before the next evaluation instead of "
+                         "overlapping it (the default runs it on RCCL's stream beside the next "
+                         "evaluation and waits for all of them inside the timed region)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="single process: evaluate only rank 0's shard of an N-way point-bucket "
                          "cut (the per-rank work of an N-GPU strong-scaling run, without the "
@@ -279,6 +283,7 @@ def main():
         returns (elapsed_s, kernel_ms_local, kernel_ms_max) maxed over ranks."""
         for _ in range(warmup):
             step()
+        se.wait_exchange()
         torch.cuda.synchronize(dev)
         if se.wait() != 0:
             raise SystemExit(f"rank {rank}: evaluation failed during warm-up")
@@ -288,6 +293,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
+        se.wait_exchange()  # every overlapped all-reduce finishes inside the timed region
         torch.cuda.synchronize(dev)
         barrier()
         elapsed = time.perf_counter() - t0
@@ -326,9 +332,18 @@ def main():
         delta = torch.full((prog.num_effective_parameters,), 1e-6, dtype=f64, device=dev)
         cand = torch.empty_like(se.state)
 
+    overlap = world > 1 and backend == "nccl" and not args.no_overlap
+    cost_ring = torch.zeros(64, dtype=f64, device=dev)  # one cost slot per in-flight step
+    ring = [0]
+
     def step():
         if args.mode == "jacobian":
-            se.evaluate(residuals=True, jacobian=True, gradient=args.gradient)
+            k = ring[0] % cost_ring.numel()
+            if overlap and k == 0:
+                se.wait_exchange()  # the slots are about to be reused
+            ring[0] += 1
+            se.evaluate(residuals=True, jacobian=True, gradient=args.gradient,
+                        cost=cost_ring[k:k + 1], overlap=overlap)
         elif args.mode == "residual":
             se.evaluate(residuals=True, jacobian=False, gradient=False)
         elif args.mode == "candidate":
@@ -460,7 +475,8 @@ def main():
                                 f"replica shards x{world}"),
                 "exchange": (None if world == 1 else
                              f"all-reduce of the cost{' and camera gradient rows' if args.gradient else ''}"
-                             f" over {'RCCL' if backend == 'nccl' else backend}"),
+                             f" over {'RCCL' if backend == 'nccl' else backend}"
+                             + (", the cost's overlapped with the next evaluation" if overlap else "")),
                 "rehearsal": (f"{world} ranks on {ndev} GPU(s), gloo" if rehearsal else None),
                 "strip_rank0": {"residuals": list(sh.residual_strip),
                                 "jacobian": [[g, g + n] for _, g, n in sh.jacobian_strips()]},

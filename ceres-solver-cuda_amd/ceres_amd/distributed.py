@@ -67,24 +67,44 @@ class ShardedEvaluator:
         self.exchange = (dist.is_available() and dist.is_initialized()
                          and dist.get_world_size(group) > 1)
         self._host_reduce = self.exchange and dist.get_backend(group) == "gloo"
+        self._pending = []
 
     # ---- evaluation -------------------------------------------------------
-    def evaluate(self, residuals=True, jacobian=True, gradient=None):
+    def evaluate(self, residuals=True, jacobian=True, gradient=None, cost=None, overlap=False):
         """One Evaluate of this rank's shard, then the exchange step.
-        Asynchronous on the rank's stream except for the all-reduce."""
+
+        The evaluation is asynchronous on the rank's stream.  The cost goes to
+        `cost` (a one-element device tensor, default self.cost).  With
+        overlap=False the all-reduce is ordered before anything queued after
+        it on the stream (torch.distributed's default).  With overlap=True
+        (RCCL only) the cost all-reduce runs on the collective stream while
+        the next evaluation proceeds; its handle is kept until
+        wait_exchange(), so each call must pass its own `cost` buffer.  The
+        gradient's camera rows are always reduced in order (the gradient
+        buffer is shared)."""
         gradient = self.gradient is not None if gradient is None else gradient
         if gradient and self.gradient is None:
             raise ValueError("ShardedEvaluator built without a gradient buffer")
+        cost = self.cost if cost is None else cost
         ptr = lambda t, want: t.data_ptr() if (t is not None and want) else None
-        self.evaluator.evaluate_device(self.state.data_ptr(), self.cost.data_ptr(),
+        self.evaluator.evaluate_device(self.state.data_ptr(), cost.data_ptr(),
                                        ptr(self.residuals, residuals),
                                        ptr(self.gradient, gradient),
                                        ptr(self.jacobian, jacobian))
         if self.exchange:
-            self._all_reduce(self.cost)
+            if overlap and not self._host_reduce:
+                self._pending.append(self.dist.all_reduce(cost, group=self.group, async_op=True))
+            else:
+                self._all_reduce(cost)
             if gradient:
                 lo, hi = self._cam_rows
                 self._all_reduce(self.gradient[lo:hi])
+
+    def wait_exchange(self):
+        """Order every overlapped all-reduce before later work on the stream."""
+        for w in self._pending:
+            w.wait()
+        self._pending = []
 
     def _all_reduce(self, t):
         if self._host_reduce:
