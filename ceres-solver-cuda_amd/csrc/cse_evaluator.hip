@@ -271,6 +271,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 14: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, true, 28>>;
     case 15: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 28>>;
     case 16: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 128>>;
+    case 17: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 1>>;
+    case 18: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 2>>;
     default: return nullptr;
   }
 }

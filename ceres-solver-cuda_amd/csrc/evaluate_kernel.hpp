@@ -378,14 +378,17 @@ __device__ __forceinline__ void ReadSegmentPieces(const double* staged, int hp, 
 //   kMinLane  at least this many doubles of LDS per lane (an occupancy
 //           limit: 28 -> 56 KiB a workgroup, 2 workgroups per CU).
 //   kAlign  the store windows' alignment unit (SectorHeadPieces), bytes.
+//   kOrder  the store tail's order: 0 F, E, residuals; 1 residuals, E, F;
+//           2 E, F, residuals.
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
-          int kAlign_ = 64>
+          int kAlign_ = 64, int kOrder_ = 0>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
   static constexpr bool kTwoRound = kTwoRound_;
   static constexpr int kMinLane = kMinLane_;
   static constexpr int kAlign = kAlign_;
+  static constexpr int kOrder = kOrder_;
 };
 // Shipped: no priority changes.  kPrio 2 was 1.5-2 % faster with the
 // library sincos and divisions (profiles/round2/s1, s3c) and 2 % slower
@@ -637,10 +640,15 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(flast), "v"(elast));
 
   // ---- every store of the wave, back to back ----
-  if (jac) {
-    SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0)>(f0, f1, q0);
-    if constexpr (kQ0 > 0) StoreNt16<0>(flast, q0[kQ0 - 1]);
+  auto store_f = [&]() {
+    if (jac) {
+      SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0)>(f0, f1, q0);
+      if constexpr (kQ0 > 0) StoreNt16<0>(flast, q0[kQ0 - 1]);
+    }
+  };
+  auto store_e = [&]() {
     if constexpr (kQ1 > 0) {
+      if (!jac) return;
       if constexpr (kLdsE) {
         SegmentStoresFrom<0, kQ1 - 1>(e0, e1, q1);
         StoreNt16<0>(elast, q1[kQ1 - 1]);
@@ -654,11 +662,26 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         static_assert(kQ1 <= 3, "E cells of at most 48 bytes");
       }
     }
-  }
-  if (a.residuals) {  // a kernel argument: a scalar branch, no VALU after the stores
-    if constexpr (kQr >= 1) StoreNt16<0>(rdst, qr[0]);
-    if constexpr (kQr >= 2) StoreNt16<16>(rdst, qr[1]);
-    if constexpr (kQr >= 3) StoreNt16<32>(rdst, qr[2]);
+  };
+  auto store_r = [&]() {
+    if (a.residuals) {  // a kernel argument: a scalar branch, no VALU after the stores
+      if constexpr (kQr >= 1) StoreNt16<0>(rdst, qr[0]);
+      if constexpr (kQr >= 2) StoreNt16<16>(rdst, qr[1]);
+      if constexpr (kQr >= 3) StoreNt16<32>(rdst, qr[2]);
+    }
+  };
+  if constexpr (T::kOrder == 1) {
+    store_r();
+    store_e();
+    store_f();
+  } else if constexpr (T::kOrder == 2) {
+    store_e();
+    store_f();
+    store_r();
+  } else {
+    store_f();
+    store_e();
+    store_r();
   }
   if constexpr (kGradF) {
     SegmentStoresFrom<0, kGQ>(cb0, cb0, gq);

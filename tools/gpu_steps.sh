@@ -68,7 +68,7 @@ for s in "$@"; do
             kind=${s%%:*}; mode=jacobian; lib=""; tag=$kind
             case "$kind" in *res) mode=residual ;; *cost) mode=cost ;; esac
             case "$kind" in abprev*) lib="--lib ceres-solver-cuda_amd/lib/libcse_prev_tuning.so" ;; esac
-            timeout -k 10 600 python -u tools/ab_bench.py --variants "${s#*:}" --rounds 3 \
+            timeout -k 10 600 python -u tools/ab_bench.py --variants "${s#*:}" --rounds ${AB_ROUNDS:-3} \
               --steps 20 --mode $mode $lib --out "$OUT/$tag.json" > "$OUT/$tag.txt" 2>&1; rc=$?
             tail -6 "$OUT/$tag.txt" ;;
     py:*)   f=${s#py:}; b=$(basename "$f" .py)
