@@ -464,7 +464,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
     ok = !bad;
   }
-  const double cost = LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1);
+  const double cost =
+      LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
   if (kJac && a.gradient != nullptr && active) {
     AddGradientSlot<NR, S0>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0, S0, r, J0);
     if constexpr (S1 > 0)

@@ -246,10 +246,13 @@ CSE_HD bool EvaluateFunctorFlat(const double* d, const double* x, double* r, dou
 
 // Loss and correction (cuda_evaluator_kernel.h:373-407 /
 // residual_block.cc:159-199) on r and the per-slot Jacobians J0 (kR x S0)
-// and J1 (kR x S1).  Returns the block cost.
+// and J1 (kR x S1).  Returns the block cost.  correct = false (a cost-only
+// evaluation: no residual or Jacobian leaves the kernel) skips the
+// Corrector, as ResidualBlock::Evaluate's early exit does when neither
+// Jacobians nor residuals are output (residual_block.cc:175-179).
 template <class K, int kLoss, bool kJac>
 CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, double* J0,
-                             double* J1) {
+                             double* J1, bool correct = true) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   double sq = 0.0;
@@ -259,6 +262,7 @@ CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, d
   if (!robust) return 0.5 * sq;
   double rho[3];
   EvaluateLoss<kLoss>(lp, sq, rho);
+  if (!kJac && !correct) return 0.5 * rho[0];
   const Corrector corr(sq, rho);
   if constexpr (kJac) {
     corr.template CorrectJacobian<NR, S0>(r, J0);
