@@ -159,6 +159,7 @@ struct Group {
   int32_t slot0_lo = 0;
   int64_t slot0_count = 0;
   int slot0_stride = 0;
+  int packed_stride = 0;  // row stride of the repacked slot-0 table (doubles)
   DevBuf<double> packed0;
   // Gradient post-pass plan per slot (affine groups with a Jacobian layout).
   struct GradPlan {
@@ -255,6 +256,15 @@ LaunchFn TuningVariant(int v, bool jac) {
     switch (v) {
       case 1: return &LaunchChunks<K, L, false, false, 2, cse::Tune<1, true>>;
       case 2: return &LaunchChunks<K, L, false, false, 2, cse::Tune<2, true>>;
+      case 20: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, true>>;
+      case 21: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, true, true>>;
+      case 22: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 1>>;
+      case 23: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, true, true, 1>>;
+      case 24: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 2>>;
+      case 25: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 3>>;
+      case 26: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16>>;
+      case 27: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 0, true>>;
+      case 28: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16, true>>;
       default: return nullptr;
     }
   }
@@ -273,6 +283,14 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 16: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 128>>;
     case 17: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 1>>;
     case 18: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 2>>;
+    case 20: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, true>>;
+    case 21: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, true, true>>;
+    case 22: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 1>>;
+    case 24: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 2>>;
+    case 25: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 3>>;
+    case 26: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16>>;
+    case 27: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 0, true>>;
+    case 28: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16, true>>;
     default: return nullptr;
   }
 }
@@ -530,6 +548,10 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
   G->slot0_lo = lo;
   G->slot0_count = (int64_t)hi - lo + 1;
   G->slot0_stride = (k.s0 + 1) & ~1;
+  G->packed_stride = cse::PackedRowDoubles(k.s0);
+#ifdef CSE_TUNING
+  if (const char* e = getenv("CSE_TUNE_CAMSTRIDE")) G->packed_stride = std::max(G->slot0_stride, atoi(e));
+#endif
   // Residuals.
   G->res_base = d->residual_layout[gidx(0)];
   for (int64_t i = 0; i < n; ++i)
@@ -594,7 +616,7 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.res_base = G.res_base;
   a.packed0 = G.packed0.p;
   a.packed0_lo = G.slot0_lo;
-  a.packed0_stride = G.slot0_stride;
+  a.packed0_stride = G.packed_stride;
   a.gindex = G.gindex.p;
   a.first = G.first;
   a.residual_layout = ev->res_layout.p;
@@ -771,9 +793,9 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
-      const int64_t total = G.slot0_count * G.slot0_stride;
+      const int64_t total = G.slot0_count * G.packed_stride;
       hipLaunchKernelGGL(cse::RepackSlot0Kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                         ev->stream, d_state, G.state_base[0], G.shape.s0, G.slot0_stride,
+                         ev->stream, d_state, G.state_base[0], G.shape.s0, G.packed_stride,
                          G.slot0_lo, G.slot0_count, G.packed0.p);
     }
     fn(a, G.num_wg, ev->stream);
@@ -988,7 +1010,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     // evaluation; worth it while the slot-0 id range is small (BAL: the
     // cameras), otherwise gather 8-byte pieces from the state directly.
     if (G.affine && G.slot0_count > 0 && G.slot0_count <= (1 << 20) &&
-        (rc = G.packed0.alloc((size_t)G.slot0_count * G.slot0_stride)))
+        (rc = G.packed0.alloc((size_t)G.slot0_count * G.packed_stride)))
       return bail(rc);
     if (G.affine && ev->has_layout) {
       const int sizes[2] = {k.s0, k.s1};

@@ -182,33 +182,97 @@ __device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 i
 }
 
 // The same with slot 0 fetched by LDS-DMA (global_load_lds_dwordx4) from
-// the 16-byte-aligned repacked table: piece p (16 B) of the wave's 64
+// the line-aligned repacked table: piece p (16 B) of the wave's 64
 // blocks by lane p % 64 of load p / 64; the hardware writes each lane's
 // 16 B at lds + 16 * p, so the pieces land in block order without passing
 // through VGPRs.  The once-read streams (ids, observations, points) load
 // non-temporally (-1.3 %, profiles/r02).
-template <class K>
+// Tuning build: kStride (doubles, 0 = PackedRowDoubles) is the table's row
+// stride, which the host must have repacked with; kOwn: each lane fetches
+// its own block's pieces (no bpermute, 64 rows per instruction) into
+// piece-major LDS.
+template <class K, int kStride = 0, bool kOwn = false>
 __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int2 id,
                                               AffineInputs<K>* in, double* lds, int lane) {
   using Tr = KindTraits<K>;
   constexpr int S0 = Tr::S0;
   constexpr int S0p = (S0 + 1) & ~1;  // doubles per block in the packed table
   constexpr int kPieces = S0p / 2;    // 16-byte pieces per block
+  constexpr int kRow = kStride ? kStride : PackedRowDoubles(S0);
   const int cid_own = id.x - a.packed0_lo;
 #pragma unroll
   for (int k = 0; k < kPieces; ++k) {
-    const int p = k * kWave + lane;
-    const int t = p / kPieces, q = p - t * kPieces;
-    const int cid = __shfl(cid_own, t, kWave);
-    const double* src = a.packed0 + (int64_t)S0p * cid + 2 * q;
-    __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
+    if constexpr (kOwn) {
+      const double* src = a.packed0 + (int64_t)kRow * cid_own + 2 * k;
+      __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
+    } else {
+      const int p = k * kWave + lane;
+      const int t = p / kPieces, q = p - t * kPieces;
+      const int cid = __shfl(cid_own, t, kWave);
+      const double* src = a.packed0 + (int64_t)kRow * cid + 2 * q;
+      __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
+    }
   }
   GatherDataAndSlot1<K, true>(a, i, id, in);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+  if constexpr (kOwn) {
 #pragma unroll
-  for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+    for (int k = 0; k < S0; ++k) in->x0[k] = lds[2 * kWave * (k / 2) + 2 * lane + (k & 1)];
+  } else {
+#pragma unroll
+    for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+  }
   __builtin_amdgcn_wave_barrier();
+  in->id0 = id.x;
+  in->id1 = id.y;
+}
+
+// Tuning build: the observation load issued before the ids are waited for
+// (kEarlyObs), and optionally slot 0 straight into registers from the
+// repacked table, 16 bytes a load (kRegGather).
+template <class K, bool kReg>
+__device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 id,
+                                            AffineInputs<K>* in, double* lds, int lane) {
+  using Tr = KindTraits<K>;
+  constexpr int S0 = Tr::S0, S1 = Tr::S1, D = Tr::D;
+  constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kPieces = S0p / 2;
+  static_assert(D == 2, "observation pairs");
+  const double obs_x = __builtin_nontemporal_load(a.data + 2 * i);
+  const double obs_y = __builtin_nontemporal_load(a.data + 2 * i + 1);
+  const int cid_own = id.x - a.packed0_lo;
+  if constexpr (kReg) {
+    const double2* src = reinterpret_cast<const double2*>(a.packed0 + (int64_t)S0p * cid_own);
+    double2 v[kPieces];
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) v[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < S0; ++k) in->x0[k] = (k & 1) ? v[k / 2].y : v[k / 2].x;
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPieces; ++k) {
+      const int p = k * kWave + lane;
+      const int t = p / kPieces, q = p - t * kPieces;
+      const int cid = __shfl(cid_own, t, kWave);
+      const double* src = a.packed0 + (int64_t)S0p * cid + 2 * q;
+      __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
+    }
+  }
+  if constexpr (S1 > 0) {
+    const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
+#pragma unroll
+    for (int k = 0; k < S1; ++k) in->x1[k] = __builtin_nontemporal_load(p1 + k);
+  }
+  in->d[0] = obs_x;
+  in->d[1] = obs_y;
+  if constexpr (!kReg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+    __builtin_amdgcn_wave_barrier();
+  }
   in->id0 = id.x;
   in->id1 = id.y;
 }
@@ -380,8 +444,20 @@ __device__ __forceinline__ void ReadSegmentPieces(const double* staged, int hp, 
 //   kAlign  the store windows' alignment unit (SectorHeadPieces), bytes.
 //   kOrder  the store tail's order: 0 F, E, residuals; 1 residuals, E, F;
 //           2 E, F, residuals.
+//   kEarlyObs  issue the observation load with the ids load, before the
+//           ids are waited for (the camera and point loads depend on them).
+//   kRegGather slot 0 loaded lane by lane from the repacked table into
+//           registers (no bpermute, no LDS round trip) instead of LDS-DMA.
+//   kDiag   diagnostic (wrong results by design): 1 replaces the functor by
+//           a few additions of its inputs -- the memory path's floor; 2
+//           reads every lane's slot-0 block from the first table row (a
+//           broadcast, no gather) -- the camera gather's cost; 3 both.
+//   kCamStride the repacked slot-0 table's row stride in doubles (0:
+//           PackedRowDoubles; the host repacks at $CSE_TUNE_CAMSTRIDE).
+//   kDmaOwn  LDS-DMA of each lane's own row (GatherCoopDma kOwn).
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
-          int kAlign_ = 64, int kOrder_ = 0>
+          int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
+          int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -389,6 +465,11 @@ struct Tune {
   static constexpr int kMinLane = kMinLane_;
   static constexpr int kAlign = kAlign_;
   static constexpr int kOrder = kOrder_;
+  static constexpr bool kEarlyObs = kEarlyObs_;
+  static constexpr bool kRegGather = kRegGather_;
+  static constexpr int kDiag = kDiag_;
+  static constexpr int kCamStride = kCamStride_;
+  static constexpr bool kDmaOwn = kDmaOwn_;
 };
 // Shipped: no priority changes.  kPrio 2 was 1.5-2 % faster with the
 // library sincos and divisions (profiles/round2/s1, s3c) and 2 % slower
@@ -452,13 +533,38 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     } else {
       id = LoadIds<K>(a, i);
     }
-    GatherCoopDma<K>(a, i, id, &in, st, lane);
+    if constexpr (T::kDiag >= 2) {
+      GatherDataAndSlot1<K, true>(a, i, id, &in);
+      const double* row = a.packed0;
+#pragma unroll
+      for (int k = 0; k < S0; ++k) in.x0[k] = row[k];
+      in.id0 = id.x;
+      in.id1 = id.y;
+    } else if constexpr (T::kEarlyObs || T::kRegGather) {
+      GatherEarly<K, T::kRegGather>(a, i, id, &in, st, lane);
+    } else {
+      GatherCoopDma<K, T::kCamStride, T::kDmaOwn>(a, i, id, &in, st, lane);
+    }
   } else {
     GatherCoop<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
   }
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(0);
   double r[NR], J0[NR * S0], J1[NR * S1p];
-  bool ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
+  bool ok;
+  if constexpr (T::kDiag == 1 || T::kDiag == 3) {
+    double t = in.x1[0] + in.x1[S1 > 1 ? 1 : 0];
+#pragma unroll
+    for (int k = 0; k < S0; ++k) t += in.x0[k];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) r[k] = in.d[k < Tr::D ? k : 0] + t;
+#pragma unroll
+    for (int k = 0; k < NR * S0; ++k) J0[k] = t * (k + 1);
+#pragma unroll
+    for (int k = 0; k < NR * S1p; ++k) J1[k] = t * (k + 2);
+    ok = true;
+  } else {
+    ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
+  }
   if (ok && a.check_finite) {
     bool bad = AnyNonFinite<NR>(r);
     if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
@@ -471,11 +577,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (S1 > 0)
       AddGradientSlot<NR, S1p>(a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1, S1, r, J1);
   }
-  // The wave's cost (fixed xor-butterfly order) and failure flag, before
+  // The wave's cost (WaveSumLane0: a fixed order) and failure flag, before
   // any store is queued.
-  double wsum = active ? cost : 0.0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
+  const double wsum = WaveSumLane0(active ? cost : 0.0);
   const bool failed = __ballot(active && !ok) != 0;
   int* status_dst = a.status;
   static_assert(!kGradF || kJac, "fused gradient: Jacobian kernels only");
@@ -877,9 +981,7 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const Group
   }
   // One partial per wave (the wave's 64 blocks are the affine kernels'
   // chunk, so both paths sum the same partials in the same order).
-  double w = cost;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off, kWave);
+  const double w = WaveSumLane0(cost);
   if ((threadIdx.x & (kWave - 1)) == 0)
     a.partials[(int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave] = w;
 }

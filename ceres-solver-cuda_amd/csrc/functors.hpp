@@ -24,11 +24,76 @@ namespace cse {
     return Evaluate(d, x, x + kSize0, r);                                    \
   }
 
+// The Rodrigues factors as functions of u = theta^2:
+//   s(u) = sin(theta) / theta,   c(u) = (1 - cos(theta)) / theta^2,
+// and their u-derivatives, from their Taylor series (coefficients
+// (-1)^n / (2n+1)! and (-1)^n / (2n+2)!, rounded to double).  For
+// 0 <= u <= 1 the terms fall by a factor u / 6 or more and the first one
+// left out is below 1e-17 of the sum, so each is within an ulp or two.
+CSE_HD void RodriguesFactors(double u, double* s, double* c, double* ds, double* dc) {
+  *s = 1.0 + u * (-0.16666666666666666 + u * (0.0083333333333333332 + u * (-0.00019841269841269841 +
+       u * (2.7557319223985893e-06 + u * (-2.505210838544172e-08 + u * (1.6059043836821613e-10 +
+       u * (-7.6471637318198164e-13 + u * 2.8114572543455206e-15)))))));
+  *c = 0.5 + u * (-0.041666666666666664 + u * (0.0013888888888888889 + u * (-2.4801587301587302e-05 +
+       u * (2.7557319223985888e-07 + u * (-2.08767569878681e-09 + u * (1.1470745597729725e-11 +
+       u * (-4.7794773323873853e-14 + u * 1.5619206968586225e-16)))))));
+  *ds = -0.16666666666666666 + u * (0.016666666666666666 + u * (-0.00059523809523809529 +
+        u * (1.1022927689594357e-05 + u * (-1.2526054192720859e-07 + u * (9.6354263020929685e-10 +
+        u * (-5.3530146122738714e-12 + u * 2.2491658034764165e-14))))));
+  *dc = -0.041666666666666664 + u * (0.0027777777777777779 + u * (-7.4404761904761911e-05 +
+        u * (1.1022927689594355e-06 + u * (-1.043837849393405e-08 + u * (6.882447358637835e-11 +
+        u * (-3.3456341326711696e-13 + u * 1.249536557486898e-15))))));
+}
+CSE_HD void RodriguesFactors(double u, double* s, double* c) {
+  double ds, dc;
+  RodriguesFactors(u, s, c, &ds, &dc);  // the derivatives are dead code here
+}
+template <int N>
+CSE_HD void RodriguesFactors(const Jet<N>& u, Jet<N>* s, Jet<N>* c) {
+  double ds, dc;
+  RodriguesFactors(u.a, &s->a, &c->a, &ds, &dc);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    s->v[i] = ds * u.v[i];
+    c->v[i] = dc * u.v[i];
+  }
+}
+
 // y = R(angle_axis) x  (include/ceres/rotation.h:830-899): Rodrigues away
 // from theta == 0, the first-order form R = I + hat(w) exactly at zero so
 // Jets still carry the right derivatives.
+//
+// On the device, when every lane of the wave has theta^2 <= 1 (rotations of
+// up to 57 degrees, the usual BAL camera; a wave-uniform ballot, so no wave
+// runs both forms), the same rotation is evaluated as
+//   R x = x + s(theta^2) (w x x) + c(theta^2) (w x (w x x)),  w = angle_axis,
+// Rodrigues' formula with sin(theta)/theta and (1 - cos(theta))/theta^2 as
+// series in theta^2 (RodriguesFactors): no square root, no division, no
+// sine or cosine, and the cross products of the seeded Jets carry their
+// partials as plain copies.  At theta == 0 it is exactly the reference's
+// first-order form (s = 1, c = 1/2, and the c term vanishes with its
+// derivatives), so both branches of the reference are covered.
 template <typename T>
 CSE_HD void AngleAxisRotatePoint(const T aa[3], const T pt[3], T out[3]) {
+#ifdef __HIP_DEVICE_COMPILE__
+  {
+    const T u = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+    if (__builtin_amdgcn_ballot_w64(!(value_of(u) <= 1.0)) == 0) {
+      T s, c;
+      RodriguesFactors(u, &s, &c);
+      const T q[3] = {aa[1] * pt[2] - aa[2] * pt[1],
+                      aa[2] * pt[0] - aa[0] * pt[2],
+                      aa[0] * pt[1] - aa[1] * pt[0]};
+      const T m[3] = {aa[1] * q[2] - aa[2] * q[1],
+                      aa[2] * q[0] - aa[0] * q[2],
+                      aa[0] * q[1] - aa[1] * q[0]};
+      out[0] = pt[0] + s * q[0] + c * m[0];
+      out[1] = pt[1] + s * q[1] + c * m[1];
+      out[2] = pt[2] + s * q[2] + c * m[2];
+      return;
+    }
+  }
+#endif
   const T theta = jhypot(aa[0], aa[1], aa[2]);
   if (value_of(theta) != 0.0) {
     T sintheta, costheta;

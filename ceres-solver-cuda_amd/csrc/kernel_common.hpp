@@ -47,11 +47,12 @@ struct GroupArgs {
   int64_t res_base;
   int64_t jac_base[2][3];
   int64_t jac_stride[2];
-  // Slot-0 parameter blocks repacked at a 16-byte-aligned stride (the
-  // affine path's cooperative LDS-DMA gather; see RepackSlot0Kernel).
+  // Slot-0 parameter blocks repacked at a line-aligned stride (the affine
+  // path's cooperative LDS-DMA gather; see RepackSlot0Kernel and
+  // PackedRowDoubles).
   const double* packed0;
   int32_t packed0_lo;
-  int32_t packed0_stride;  // doubles per block, even
+  int32_t packed0_stride;  // doubles per row: PackedRowDoubles(S0)
   // Table policy.
   const int64_t* gindex;
   int64_t first;
@@ -124,6 +125,17 @@ struct TestOnly<K, decltype((void)K::kTestOnly)> {
   static constexpr bool value = K::kTestOnly;
 };
 
+// Row stride (doubles) of the repacked slot-0 table that the LDS-DMA gather
+// reads: the block's size rounded up to 16 bytes and then to a power of two
+// up to 128 bytes, so that no row straddles a 128-byte L2 line (16 doubles
+// for the 9-double BAL camera).  Each DMA instruction then touches one line
+// per row instead of 1.5 on average: the residual-only evaluation of
+// problem-13682 went from 0.487 to 0.420 ms (profiles/round2/s4e).
+constexpr int PackedRowDoubles(int s) {
+  const int p = (s + 1) & ~1;
+  return p <= 2 ? 2 : p <= 4 ? 4 : p <= 8 ? 8 : p <= 16 ? 16 : p;
+}
+
 // Any of x[0..n) NaN or infinite?  An integer test on the exponent field:
 // the TU is compiled with -ffinite-math-only, which would fold isfinite().
 template <int kCount>
@@ -146,6 +158,34 @@ CSE_HD bool AnyImpossible(const double* x) {
   for (int i = 0; i < kCount; ++i)
     any = any || __builtin_bit_cast(uint64_t, x[i]) == __builtin_bit_cast(uint64_t, kImpossibleValue);
   return any;
+}
+
+// x of lane (lane ^ kOff), kOff < 32, by ds_swizzle in bit mode (and mask
+// 0x1f, xor mask kOff): no address VGPRs and no range checks, where
+// __shfl_xor costs four VALU instructions per step.
+template <int kOff>
+__device__ __forceinline__ double SwizzleXor(double x) {
+  static_assert(kOff > 0 && kOff < 32, "ds_swizzle bit mode acts within 32 lanes");
+  constexpr int kPattern = (kOff << 10) | 0x1f;
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(x), kPattern);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(x), kPattern);
+  return __hiloint2double(hi, lo);
+}
+
+// The sum of v over the wave's 64 lanes, in lane 0, in a fixed order:
+// butterflies over lane ^ 1, 2, 4, 8, 16 (each 32-lane half's sum in all of
+// its lanes), then lane 0's half plus lane 32's.  Every lane must be active.
+// The affine and the table kernels both use it, so their per-wave cost
+// partials are bit-identical.
+__device__ __forceinline__ double WaveSumLane0(double v) {
+  v += SwizzleXor<1>(v);
+  v += SwizzleXor<2>(v);
+  v += SwizzleXor<4>(v);
+  v += SwizzleXor<8>(v);
+  v += SwizzleXor<16>(v);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 32);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 32);
+  return v + __hiloint2double(hi, lo);
 }
 
 // Deterministic workgroup sum: xor-butterfly inside each wave, then the

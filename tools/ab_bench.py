@@ -44,7 +44,9 @@ def main():
     ap.add_argument("--mode", default="jacobian", choices=["jacobian", "residual", "cost"])
     args = ap.parse_args()
     import torch
-    variants = [int(v) for v in args.variants.split(",")]
+    # "26s16": variant 26 with the slot-0 table repacked at a 16-double stride
+    # (CSE_TUNE_CAMSTRIDE, read when the evaluator is created).
+    variants = args.variants.split(",")
     loss = {"huber": ca.Loss.huber(1.0), "trivial": ca.Loss.trivial()}[args.loss]
     t0 = time.time()
     prog = bal.synthetic_program(args.config, loss=loss)
@@ -61,7 +63,12 @@ def main():
     bytes_ = None
     for rnd in range(args.rounds):
         for v in variants:
-            os.environ["CSE_TUNE_VARIANT"] = str(v)
+            vv, _, cs = v.partition("s")
+            os.environ["CSE_TUNE_VARIANT"] = vv
+            if cs:
+                os.environ["CSE_TUNE_CAMSTRIDE"] = cs
+            else:
+                os.environ.pop("CSE_TUNE_CAMSTRIDE", None)
             ev = ca.Evaluator(prog, device=0, profile=True, stream=stream.cuda_stream)
             info = ev.info()
             bytes_ = {"jacobian": info.bytes_jacobian_eval, "residual": info.bytes_residual_eval,
