@@ -291,6 +291,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 26: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16>>;
     case 27: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 0, true>>;
     case 28: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16, true>>;
+    case 29: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 4>>;
+    case 30: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 5>>;
     default: return nullptr;
   }
 }

@@ -243,7 +243,8 @@ __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 
   const double obs_y = __builtin_nontemporal_load(a.data + 2 * i + 1);
   const int cid_own = id.x - a.packed0_lo;
   if constexpr (kReg) {
-    const double2* src = reinterpret_cast<const double2*>(a.packed0 + (int64_t)S0p * cid_own);
+    const double2* src =
+        reinterpret_cast<const double2*>(a.packed0 + (int64_t)PackedRowDoubles(S0) * cid_own);
     double2 v[kPieces];
 #pragma unroll
     for (int k = 0; k < kPieces; ++k) v[k] = src[k];
@@ -255,7 +256,7 @@ __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 
       const int p = k * kWave + lane;
       const int t = p / kPieces, q = p - t * kPieces;
       const int cid = __shfl(cid_own, t, kWave);
-      const double* src = a.packed0 + (int64_t)S0p * cid + 2 * q;
+      const double* src = a.packed0 + (int64_t)PackedRowDoubles(S0) * cid + 2 * q;
       __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
     }
   }
@@ -451,7 +452,8 @@ __device__ __forceinline__ void ReadSegmentPieces(const double* staged, int hp, 
 //   kDiag   diagnostic (wrong results by design): 1 replaces the functor by
 //           a few additions of its inputs -- the memory path's floor; 2
 //           reads every lane's slot-0 block from the first table row (a
-//           broadcast, no gather) -- the camera gather's cost; 3 both.
+//           broadcast, no gather) -- the camera gather's cost; 3 both; 4
+//           no Jacobian stores (residuals and partials only); 5 no E stores.
 //   kCamStride the repacked slot-0 table's row stride in doubles (0:
 //           PackedRowDoubles; the host repacks at $CSE_TUNE_CAMSTRIDE).
 //   kDmaOwn  LDS-DMA of each lane's own row (GatherCoopDma kOwn).
@@ -533,14 +535,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     } else {
       id = LoadIds<K>(a, i);
     }
-    if constexpr (T::kDiag >= 2) {
+    if constexpr (T::kDiag == 2 || T::kDiag == 3) {
       GatherDataAndSlot1<K, true>(a, i, id, &in);
       const double* row = a.packed0;
 #pragma unroll
       for (int k = 0; k < S0; ++k) in.x0[k] = row[k];
       in.id0 = id.x;
       in.id1 = id.y;
-    } else if constexpr (T::kEarlyObs || T::kRegGather) {
+    } else if constexpr (T::kEarlyObs || T::kRegGather ||
+                         (!kJac && Tr::D == 2 && Tr::NB == 2 && T::kCamStride == 0 && !T::kDmaOwn)) {
+      // Residual-only and cost-only evaluations issue the observation load
+      // with the ids load (1.5-2 % faster, profiles/round2/s4h; the
+      // Jacobian kernel is 4 % slower that way, s4c).
       GatherEarly<K, T::kRegGather>(a, i, id, &in, st, lane);
     } else {
       GatherCoopDma<K, T::kCamStride, T::kDmaOwn>(a, i, id, &in, st, lane);
@@ -746,12 +752,14 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 
   // ---- every store of the wave, back to back ----
   auto store_f = [&]() {
+    if constexpr (T::kDiag == 4) return;
     if (jac) {
       SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0)>(f0, f1, q0);
       if constexpr (kQ0 > 0) StoreNt16<0>(flast, q0[kQ0 - 1]);
     }
   };
   auto store_e = [&]() {
+    if constexpr (T::kDiag == 4 || T::kDiag == 5) return;
     if constexpr (kQ1 > 0) {
       if (!jac) return;
       if constexpr (kLdsE) {
