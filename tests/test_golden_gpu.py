@@ -76,10 +76,25 @@ def _check(rows, r, g, j, cost, fmt):
     assert abs(cost - total) <= 1e-12 * abs(total)
 
 
+def _theta2(case):
+    # angle-axis functors only (the quaternion kind has 10 camera values)
+    cam = case["camera"]
+    return sum(v * v for v in cam[:3]) if len(cam) in (7, 9) else 0.0
+
+
 @pytest.mark.parametrize("fmt", [ca.COMPRESSED_ROW, ca.BLOCK_SPARSE])
-def test_golden_vectors_on_gpu(gpu, fmt):
+@pytest.mark.parametrize("angles", ["all", "small", "large"])
+def test_golden_vectors_on_gpu(gpu, fmt, angles):
+    # "small" keeps the cases with theta^2 <= 1 (every wave takes the series
+    # form of AngleAxisRotatePoint), "large" those with theta^2 > 1 (the
+    # reference's form); "all" mixes them in one wave.
     with open(GOLDEN) as fh:
         cases = json.load(fh)["cases"]
+    if angles == "small":
+        cases = [c for c in cases if _theta2(c) <= 1.0]
+    elif angles == "large":
+        cases = [c for c in cases if _theta2(c) > 1.0]
+    assert cases
     prog, rows = _program(cases, fmt)
     ev = ca.Evaluator(prog)
     try:
