@@ -204,6 +204,13 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
+// The shipped BSM Jacobian kernel of two-slot kinds (4 waves per SIMD).
+template <class K, int L, int Co>
+void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRound<K, L, Co>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
+}
+
 // The affine kernel with the fused gradient (Snavely groups, gradient_mode 0).
 template <int L, bool Crs>
 void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
@@ -224,6 +231,10 @@ LaunchFn PickFused(int loss, int policy) {
 // table (dma = true) or by 8-byte pieces straight from the state.
 template <class K, int L, bool Crs>
 LaunchFn PickAffine(bool jac, bool dma) {
+  if constexpr (!Crs && cse::kTwoRoundBsm<K>) {
+    // (the 8-byte-piece gather of kCoop 1 would spill at 128 VGPRs)
+    if (jac && dma) return &LaunchTwoRound<K, L, 2>;
+  }
   if (dma) return jac ? &LaunchChunks<K, L, true, Crs, 2> : &LaunchChunks<K, L, false, Crs, 2>;
   return jac ? &LaunchChunks<K, L, true, Crs, 1> : &LaunchChunks<K, L, false, Crs, 1>;
 }

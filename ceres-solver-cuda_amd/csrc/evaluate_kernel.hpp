@@ -473,10 +473,18 @@ struct Tune {
   static constexpr int kCamStride = kCamStride_;
   static constexpr bool kDmaOwn = kDmaOwn_;
 };
-// Shipped: no priority changes.  kPrio 2 was 1.5-2 % faster with the
-// library sincos and divisions (profiles/round2/s1, s3c) and 2 % slower
-// once the functor's FP64 work shrank (profiles/round2/s3d).
-using ShippedTune = Tune<0, true>;
+// Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
+// sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
+// functor's FP64 work shrank, s3d); two-round E/F staging (9 KiB of LDS a
+// wave), which with the kernel held to 128 VGPRs (EvaluateAffineChunksTwoRound)
+// gives 4 waves per SIMD instead of 3.  That was neutral with the heavier
+// functor (s3i, s3j) and is 2.5 % faster with the series rotation (s4n).
+using ShippedTune = Tune<0, true, true>;
+
+// Does the shipped BSM Jacobian kernel of kind K stage in two rounds (and so
+// fit 4 workgroups per CU)?
+template <class K>
+constexpr bool kTwoRoundBsm = KindTraits<K>::S1 > 0;
 
 // The hot kernel: one 64-block chunk per wave, every output store issued
 // back to back at the very end of the wave (see the store primitives in
@@ -828,6 +836,14 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T = ShippedTune>
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const GroupArgs a) {
   AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T>(a);
+}
+
+// The shipped BSM Jacobian kernel of two-slot kinds: two-round staging (36
+// KiB of LDS a workgroup, 4 per CU) held to 4 waves per SIMD (128 VGPRs).
+template <class K, int kLoss, int kCoop>
+__global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound(const GroupArgs a) {
+  static_assert(kTwoRoundBsm<K>, "two-slot kinds");
+  AffineChunkBody<K, kLoss, true, false, kCoop, false, ShippedTune>(a);
 }
 
 // The same held to at least kMinWaves waves per SIMD (a register bound:

@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--loss", default="huber")
     ap.add_argument("--out", default=None)
     ap.add_argument("--lib", default=None, help="tuning library to load (default lib/libcse_tuning.so)")
-    ap.add_argument("--mode", default="jacobian", choices=["jacobian", "residual", "cost"])
+    ap.add_argument("--mode", default="jacobian", choices=["jacobian", "gradient", "residual", "cost"])
     args = ap.parse_args()
     import torch
     # "26s16": variant 26 with the slot-0 table repacked at a 16-double stride
@@ -57,6 +57,7 @@ def main():
     cost = torch.zeros(1, dtype=f64, device=dev)
     res = torch.empty(prog.num_residuals, dtype=f64, device=dev)
     jac = torch.empty(prog.num_jacobian_values, dtype=f64, device=dev)
+    grad = torch.empty(prog.num_effective_parameters, dtype=f64, device=dev)
     stream = torch.cuda.current_stream(dev)
     ref_hash = None
     times = {v: [] for v in variants}
@@ -72,11 +73,13 @@ def main():
             ev = ca.Evaluator(prog, device=0, profile=True, stream=stream.cuda_stream)
             info = ev.info()
             bytes_ = {"jacobian": info.bytes_jacobian_eval, "residual": info.bytes_residual_eval,
+                      "gradient": info.bytes_jacobian_eval + 8 * prog.num_effective_parameters,
                       "cost": info.bytes_residual_eval - 8 * prog.num_residuals}[args.mode]
             rp = res.data_ptr() if args.mode != "cost" else None
-            jp = jac.data_ptr() if args.mode == "jacobian" else None
+            jp = jac.data_ptr() if args.mode in ("jacobian", "gradient") else None
+            gp = grad.data_ptr() if args.mode == "gradient" else None
             for _ in range(3):
-                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, None, jp)
+                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, gp, jp)
             assert ev.wait() == 0
             if rnd == 0:
                 h = hashlib.sha1()
@@ -84,6 +87,8 @@ def main():
                 h.update(jac[:: 97].cpu().numpy().tobytes())
                 h.update(jac[-100000:].cpu().numpy().tobytes())
                 h.update(cost.cpu().numpy().tobytes())
+                if args.mode == "gradient":
+                    h.update(grad.cpu().numpy().tobytes())
                 digest = h.hexdigest()
                 if ref_hash is None:
                     ref_hash = digest
@@ -91,7 +96,7 @@ def main():
                 print(f"# variant {v}: outputs {'identical' if same else 'DIFFER'}", flush=True)
             ev.reset_kernel_stats()
             for _ in range(args.steps):
-                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, None, jp)
+                ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, gp, jp)
             assert ev.wait() == 0
             _, total, n = ev.kernel_stats()
             ev.close()
