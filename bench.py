@@ -70,8 +70,10 @@ def parse():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--gradient", action="store_true",
                     help="the headline step also produces the gradient J^T r")
-    ap.add_argument("--gradient-mode", type=int, default=0, choices=[0, 1, 2],
-                    help="cse_options.gradient_mode: 0 fused (default), 1 post-pass, 2 atomics")
+    ap.add_argument("--gradient-mode", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="cse_options.gradient_mode: 0 fused, camera rows re-evaluated in camera "
+                         "order (default), 1 post-pass, 2 atomics, 3 fused with block-order "
+                         "camera contributions")
     ap.add_argument("--mode", default="jacobian",
                     choices=["jacobian", "residual", "candidate", "spmv", "cgnr", "schur"],
                     help="jacobian: residual+Jacobian evaluation (the headline metric); "

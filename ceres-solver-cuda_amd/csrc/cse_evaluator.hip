@@ -171,6 +171,7 @@ struct Group {
     DevBuf<int64_t> off;
     // wave mode: chunks of at most cse::kGradChunk blocks
     DevBuf<int64_t> chunk_begin, chunk_off;
+    DevBuf<int32_t> chunk_pb;  // parameter block (id) of each chunk
     DevBuf<double> chunk_partial;
     int64_t nchunks = 0;
   } grad[2];
@@ -178,6 +179,10 @@ struct Group {
   // boundary entries and slot-0 contributions (allocated on first use).
   bool fuse_ok = false;
   DevBuf<double> gside, gcontrib;
+  // Slot-0-sorted functor data and slot-1 ids (CameraGradientKernel; built
+  // on first use).
+  DevBuf<double> sdata;
+  DevBuf<int32_t> sid1;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -211,10 +216,17 @@ void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
-// The affine kernel with the fused gradient (Snavely groups, gradient_mode 0).
+// The affine kernel with the fused gradient (Snavely groups): with the
+// slot-0 contributions (gradient_mode 3) or points only (gradient_mode 0,
+// slot 0 from CameraGradientKernel).
 template <int L, bool Crs>
 void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<cse::SnavelyKind, L, Crs>),
+                     dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
+}
+template <int L, bool Crs>
+void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<cse::SnavelyKind, L, Crs>),
                      dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
 }
 
@@ -224,6 +236,14 @@ LaunchFn PickFused(int loss, int policy) {
     case CSE_LOSS_HUBER: return crs ? &LaunchFused<cse::kLossHuber, true> : &LaunchFused<cse::kLossHuber, false>;
     case CSE_LOSS_CAUCHY: return crs ? &LaunchFused<cse::kLossCauchy, true> : &LaunchFused<cse::kLossCauchy, false>;
     default: return crs ? &LaunchFused<cse::kLossTrivial, true> : &LaunchFused<cse::kLossTrivial, false>;
+  }
+}
+LaunchFn PickFusedPoints(int loss, int policy) {
+  const bool crs = policy == kAffineCrs;
+  switch (loss) {
+    case CSE_LOSS_HUBER: return crs ? &LaunchFusedPoints<cse::kLossHuber, true> : &LaunchFusedPoints<cse::kLossHuber, false>;
+    case CSE_LOSS_CAUCHY: return crs ? &LaunchFusedPoints<cse::kLossCauchy, true> : &LaunchFusedPoints<cse::kLossCauchy, false>;
+    default: return crs ? &LaunchFusedPoints<cse::kLossTrivial, true> : &LaunchFusedPoints<cse::kLossTrivial, false>;
   }
 }
 
@@ -469,9 +489,13 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
   // Chunks: the wave-mode post-pass and the fused gradient's slot-0 pass.
   if (!sorted) {
     std::vector<int64_t> begin, coff(count + 1, 0);
+    std::vector<int32_t> cpb;
     for (int64_t p = 0; p < count; ++p) {
       coff[p] = (int64_t)begin.size();
-      for (int64_t q = off[p]; q < off[p + 1]; q += cse::kGradChunk) begin.push_back(q);
+      for (int64_t q = off[p]; q < off[p + 1]; q += cse::kGradChunk) {
+        begin.push_back(q);
+        cpb.push_back((int32_t)(lo + p));
+      }
     }
     coff[count] = (int64_t)begin.size();
     plan->nchunks = (int64_t)begin.size();
@@ -480,6 +504,7 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
     begin.push_back(n);
     if ((rc = plan->chunk_begin.upload(begin.data(), begin.size(), s))) return rc;
     if ((rc = plan->chunk_off.upload(coff.data(), coff.size(), s))) return rc;
+    if (!cpb.empty() && (rc = plan->chunk_pb.upload(cpb.data(), cpb.size(), s))) return rc;
     const int size = j == 0 ? k.s0 : k.s1;
     if ((rc = plan->chunk_partial.alloc((size_t)std::max<int64_t>(1, plan->nchunks) * size)))
       return rc;
@@ -688,6 +713,72 @@ int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
   return CSE_OK;
 }
 
+// gradient_mode 0: the slot-1 boundary entries as above, and the slot-0
+// sums by re-evaluation in camera order (CameraGradientKernel), then
+// GradientChunkReduceKernel.  The sorted inputs are built on first use.
+int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, double* out,
+                         hipStream_t s) {
+  const Group::GradPlan& P = G.grad[0];
+  const int D = G.shape.data;
+  int rc;
+  if (G.sdata.p == nullptr) {
+    if ((rc = G.sdata.alloc((size_t)G.n * D))) return rc;
+    if ((rc = G.sid1.alloc((size_t)G.n))) return rc;
+    if (D != 2) return Fail(CSE_ERR_UNSUPPORTED, "camera-order gradient: 2 data doubles per block");
+    hipLaunchKernelGGL((cse::SortSlot0InputsKernel<2>),
+                       dim3((unsigned)((G.n + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                       dim3(cse::kBlockThreads), 0, s, G.ids.p, G.data.p, P.perm.p, G.n, G.sdata.p,
+                       G.sid1.p);
+    CSE_HIP(hipGetLastError());
+  }
+  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
+  hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
+                     dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
+  cse::CamGradArgs cg{};
+  cg.state = state;
+  cg.state_base0 = G.state_base[0];
+  cg.state_base1 = G.state_base[1];
+  cg.sdata = G.sdata.p;
+  cg.sid1 = G.sid1.p;
+  cg.chunk_pb = P.chunk_pb.p;
+  cg.chunk_begin = P.chunk_begin.p;
+  cg.partial = P.chunk_partial.p;
+  cg.nchunks = P.nchunks;
+  cg.loss.a = G.loss.a;
+  cg.loss.scale = G.loss.scale;
+  cg.loss.scaled = G.loss.scaled;
+  cg.apply_loss = ev->opts.apply_loss_function;
+  const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
+  if (P.nchunks > 0) {
+    using K = cse::SnavelyKind;
+    switch (G.loss.kind) {
+      case CSE_LOSS_HUBER:
+        hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossHuber>), grid,
+                           dim3(cse::kBlockThreads), 0, s, cg);
+        break;
+      case CSE_LOSS_CAUCHY:
+        hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossCauchy>), grid,
+                           dim3(cse::kBlockThreads), 0, s, cg);
+        break;
+      default:
+        hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossTrivial>), grid,
+                           dim3(cse::kBlockThreads), 0, s, cg);
+    }
+  }
+  cse::GradArgs ga{};
+  ga.count = P.count;
+  ga.lo = P.lo;
+  ga.grad = out;
+  ga.delta_base = G.delta_base[0];
+  const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
+  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
+                     dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, ga, ch);
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
 // The implicit Schur complement's structure (cse_schur_*): one Snavely
 // group on the fused-gradient path with the BlockSparseMatrix layout, its
 // e blocks (slot 1, points) the leading columns [0, e_cols) and its f blocks
@@ -792,17 +883,19 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     // FP64 atomics (as the reference).
     bool grad_pass = d_grad && d_res && d_jac && G.affine && ev->opts.gradient_mode != 2;
     for (int j = 0; j < G.shape.nb; ++j) grad_pass = grad_pass && G.grad[j].ready;
-    const bool fused = grad_pass && G.fuse_ok && ev->opts.gradient_mode == 0;
+    const int mode = ev->opts.gradient_mode;
+    const bool fused = grad_pass && G.fuse_ok && (mode == 0 || mode == 3);
+    const bool recompute = fused && mode == 0;  // slot 0 by CameraGradientKernel
     cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
     if (fused) {
       const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
       int rc;
       if ((rc = G.gside.ensure((size_t)(2 * chunks * 4)))) return rc;
-      if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
+      if (!recompute && (rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
       a.gfused = d_grad;
       a.gside = G.gside.p;
       a.gcontrib = G.gcontrib.p;
-      fn = PickFused(G.loss.kind, G.policy);
+      fn = recompute ? PickFusedPoints(G.loss.kind, G.policy) : PickFused(G.loss.kind, G.policy);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
@@ -813,7 +906,10 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
-    if (fused) {
+    if (recompute) {
+      const int rc = LaunchCameraGradTail(ev, G, d_state, d_grad, ev->stream);
+      if (rc) return rc;
+    } else if (fused) {
       const int rc = LaunchFusedGradTail(G, d_grad, ev->stream);
       if (rc) return rc;
     } else if (grad_pass) {
@@ -1541,7 +1637,8 @@ int cse_get_info(cse_evaluator* ev, cse_info* info) {
   info->num_groups = (int32_t)ev->groups.size();
   for (auto& G : ev->groups) {
     info->num_affine_groups += G.affine ? 1 : 0;
-    info->num_fused_gradient_groups += (G.fuse_ok && ev->opts.gradient_mode == 0) ? 1 : 0;
+    info->num_fused_gradient_groups +=
+        (G.fuse_ok && (ev->opts.gradient_mode == 0 || ev->opts.gradient_mode == 3)) ? 1 : 0;
   }
   info->device = ev->device;
   info->bytes_jacobian_eval = ev->bytes_jac;

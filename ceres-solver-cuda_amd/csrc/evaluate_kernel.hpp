@@ -457,9 +457,11 @@ __device__ __forceinline__ void ReadSegmentPieces(const double* staged, int hp, 
 //   kCamStride the repacked slot-0 table's row stride in doubles (0:
 //           PackedRowDoubles; the host repacks at $CSE_TUNE_CAMSTRIDE).
 //   kDmaOwn  LDS-DMA of each lane's own row (GatherCoopDma kOwn).
+//   kNoContrib  fused gradient without the slot-0 contributions (the slot-0
+//           sums come from CameraGradientKernel instead).
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
-          int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false>
+          int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -472,6 +474,7 @@ struct Tune {
   static constexpr int kDiag = kDiag_;
   static constexpr int kCamStride = kCamStride_;
   static constexpr bool kDmaOwn = kDmaOwn_;
+  static constexpr bool kNoContrib = kNoContrib_;
 };
 // Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
 // sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
@@ -480,6 +483,8 @@ struct Tune {
 // gives 4 waves per SIMD instead of 3.  That was neutral with the heavier
 // functor (s3i, s3j) and is 2.5 % faster with the series rotation (s4n).
 using ShippedTune = Tune<0, true, true>;
+// The fused gradient's points-only form (CameraGradientKernel adds slot 0).
+using PointsOnlyTune = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true>;
 
 // Does the shipped BSM Jacobian kernel of kind K stage in two rounds (and so
 // fit 4 workgroups per CU)?
@@ -605,7 +610,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;
-      if (active) {
+      if (!T::kNoContrib && active) {
         double* cdst = a.gcontrib + (int64_t)S0p * (i0 + lane);
 #pragma unroll
         for (int cc = 0; cc < S0p; ++cc) cdst[cc] = fg.g0[cc];
@@ -702,11 +707,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   }
   // Fused gradient: the slot-0 contributions staged through the same LDS
   // (after the Jacobian pieces have been read back), the slot-1 entry.
-  constexpr int kGQ = kGradF ? FusedGrad<K>::S0p / 2 : 1;
+  constexpr bool kContrib = kGradF && !T::kNoContrib;
+  constexpr int kGQ = kContrib ? FusedGrad<K>::S0p / 2 : 1;
   static_assert(kGQ <= 8, "contribution pieces: one base register");
   cse_v4i gq[kGQ], sq[2];
   double *cb0 = nullptr, *gp = nullptr, *sp = nullptr;
   if constexpr (kGradF) {
+    sq[0] = AsV4i(fg.g1[0], fg.g1[1]);
+    sq[1] = AsV4i(fg.g1[2], fg.g1[3]);
+    gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
+    sp = a.gside + 4 * fg.entry;
+  }
+  if constexpr (kContrib) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -718,11 +730,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       const double2 v = reinterpret_cast<const double2*>(st)[j * kWave + lane];
       gq[j] = AsV4i(v.x, v.y);
     }
-    sq[0] = AsV4i(fg.g1[0], fg.g1[1]);
-    sq[1] = AsV4i(fg.g1[2], fg.g1[3]);
     cb0 = a.gcontrib + (int64_t)(2 * kGQ) * i0 + 2 * lane + 512;
-    gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
-    sp = a.gside + 4 * fg.entry;
   }
   // Residual pieces: the lane's own NR doubles (NR even).
   constexpr int kQr = NR / 2;
@@ -805,7 +813,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     store_r();
   }
   if constexpr (kGradF) {
-    SegmentStoresFrom<0, kGQ>(cb0, cb0, gq);
+    if constexpr (kContrib) SegmentStoresFrom<0, kGQ>(cb0, cb0, gq);
     if (fg.interior) {
       StoreB64At<0>(gp, fg.g1[0]);
       StoreB64At<8>(gp, fg.g1[1]);
@@ -827,7 +835,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(v_partial), "v"(v_wsum),
                "v"(flast), "v"(elast));
   if constexpr (kGradF) {
-    KeepAlive<kGQ>(gq);
+    if constexpr (kContrib) KeepAlive<kGQ>(gq);
     KeepAlive<2>(sq);
     asm volatile("" ::"v"(cb0), "v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
   }
@@ -861,6 +869,228 @@ template <class K, int kLoss, bool kCrs>
 __global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(3))) void
 EvaluateAffineChunksFused(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, kCrs, 2, true>(a);
+}
+
+// The fused gradient's points-only form: the slot-1 rows and boundary
+// entries as above, no slot-0 contributions (CameraGradientKernel computes
+// the slot-0 sums).  Without the contribution registers the BSM form fits
+// 128 VGPRs, so it runs at the two-round kernel's 4 waves per SIMD.
+template <class K, int kLoss, bool kCrs>
+__global__ __launch_bounds__(kBlockThreads, kCrs ? 3 : 4) void EvaluateAffineChunksFusedPoints(
+    const GroupArgs a) {
+  AffineChunkBody<K, kLoss, true, kCrs, 2, true, PointsOnlyTune>(a);
+}
+
+// Slot-0 (camera) part of the fused gradient, by re-evaluation in camera
+// order.  The evaluation kernel runs in block (point) order, in which a
+// camera's ~2,100 blocks are spread over the whole problem; summing their
+// J0^T r there needs a transposing round trip through HBM (2.3 GB written in
+// block order, 5.8 GB of lines gathered back in camera order at
+// problem-13682, GradientContribKernel).  Here each wave takes one chunk of
+// at most kGradChunk consecutive entries of one camera's block list and
+// evaluates those blocks again with the camera's 9 partials only (Jet<S0>,
+// the point a constant): the camera is uniform over the wave, the functor
+// data and point ids stream in camera order from a copy sorted once at
+// setup (SortSlot0InputsKernel), and only the 24-byte points are gathered
+// (a 107 MB table, mostly served from the Infinity Cache).  Per block the
+// loss and the Corrector are applied to r and J0 as in the evaluation
+// (residual_block.cc:159-199), then J0^T r is added; lanes accumulate
+// their blocks in list order and the wave sums by a fixed butterfly, so the
+// chunk partials -- and, through GradientChunkReduceKernel, the gradient --
+// are deterministic and in the same order as GradientContribKernel's.
+// The reference adds the same products with atomics
+// (cuda_evaluator_kernel.h:149-160).
+struct CamGradArgs {
+  const double* state;
+  int64_t state_base0, state_base1;
+  const double* sdata;         // [n][D] functor data, slot-0-sorted order
+  const int32_t* sid1;         // [n] slot-1 ids, same order
+  const int32_t* chunk_pb;     // [nchunks] slot-0 id of each chunk
+  const int64_t* chunk_begin;  // [nchunks + 1]
+  double* partial;             // [nchunks][S0]
+  int64_t nchunks;
+  LossParams loss;
+  int apply_loss;
+};
+
+// r and the slot-0 Jacobian (NR x S0, row-major) of one block, the slot-1
+// parameters held constant (AutoDifferentiate with only slot 0 seeded).
+template <class K>
+__device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
+                                              const double* x1, double* r, double* J0) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1;
+  Jet<S0> j0[S0], j1[S1], out[NR];
+#pragma unroll
+  for (int k = 0; k < S0; ++k) j0[k] = Jet<S0>(x0[k], k);
+#pragma unroll
+  for (int k = 0; k < S1; ++k) j1[k] = Jet<S0>(x1[k]);
+  K::Evaluate(d, j0, j1, out);
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    r[k] = out[k].a;
+#pragma unroll
+    for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+  }
+}
+
+// SnavelyReprojectionError's camera partials with the wave's camera fixed
+// (examples/snavely_reprojection_error.h:58-93).  The rotation is linear in
+// the point, so R and its three angle-axis partials are formed once per
+// wave -- column k is AngleAxisRotatePoint(aa, e_k) on Jet<3> angle-axis
+// seeds, the same Rodrigues forms as the evaluation (§3.1) -- and each
+// block's p = R X + t carries its partials as dR/dw_j X (translation: unit
+// partials); the projection and distortion then run on Jet<9> as in the
+// functor.  Against the full Jet<9> functor per block this removes the
+// per-lane Rodrigues evaluation; p differs from the functor's by rounding
+// only (R X summed as a matrix product).
+struct SnavelyCameraFrame {
+  double R[3][3];      // R[i][k]
+  double dR[3][3][3];  // dR[j][i][k] = d R[i][k] / d aa_j
+  double t[3], f, l[2];
+
+  __device__ __forceinline__ void Init(const double* cam) {
+    Jet<3> aa[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) aa[j] = Jet<3>(cam[j], j);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      Jet<3> e[3], col[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) e[i] = Jet<3>(i == k ? 1.0 : 0.0);
+      AngleAxisRotatePoint(aa, e, col);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        R[i][k] = col[i].a;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dR[j][i][k] = col[i].v[j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] = cam[3 + i];
+    f = cam[6];
+    l[0] = cam[7];
+    l[1] = cam[8];
+    // Wave-uniform: held in SGPRs (operands of the per-block FMAs), not in
+    // 84 VGPRs.
+    double* all = &R[0][0];
+    static_assert(sizeof(SnavelyCameraFrame) == 42 * sizeof(double), "frame layout");
+#pragma unroll
+    for (int k = 0; k < 42; ++k) all[k] = Uniform(all[k]);
+  }
+  static __device__ __forceinline__ double Uniform(double x) {
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(x));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(x));
+    return __hiloint2double(hi, lo);
+  }
+
+  // r (2) and J0 (2 x 9, row-major) of the block observing X.
+  __device__ __forceinline__ void Evaluate(const double* obs, const double* X, double* r,
+                                           double* J0) const {
+    Jet<9> p[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      p[i] = Jet<9>(R[i][0] * X[0] + R[i][1] * X[1] + R[i][2] * X[2] + t[i]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) p[i].v[j] = dR[j][i][0] * X[0] + dR[j][i][1] * X[1] + dR[j][i][2] * X[2];
+      p[i].v[3 + i] = 1.0;
+    }
+    const Jet<9> focal(f, 6);
+    const Jet<9> dist[2] = {Jet<9>(l[0], 7), Jet<9>(l[1], 8)};
+    Jet<9> out[2];
+    Project<true>(p, focal, dist, obs, out);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      r[k] = out[k].a;
+#pragma unroll
+      for (int c = 0; c < 9; ++c) J0[k * 9 + c] = out[k].v[c];
+    }
+  }
+};
+
+#ifndef CSE_CAMGRAD_ROTMAT
+#define CSE_CAMGRAD_ROTMAT 0
+#endif
+
+template <class K, int kLoss>
+__global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamGradArgs g) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, D = Tr::D;
+  static_assert(Tr::NB == 2 && S1 > 0, "two-slot kinds");
+  constexpr bool kFrame = CSE_CAMGRAD_ROTMAT && std::is_same<K, SnavelyKind>::value;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (cid >= g.nchunks) return;
+  const int64_t q0 = g.chunk_begin[cid], q1 = g.chunk_begin[cid + 1];
+  const double* cam = g.state + g.state_base0 + (int64_t)S0 * g.chunk_pb[cid];
+  double x0[S0];
+#pragma unroll
+  for (int k = 0; k < S0; ++k) x0[k] = cam[k];
+  SnavelyCameraFrame frame;
+  if constexpr (kFrame) frame.Init(x0);
+  double acc[S0];
+#pragma unroll
+  for (int c = 0; c < S0; ++c) acc[c] = 0.0;
+  // Two blocks per lane and step: both blocks' loads are in flight before
+  // either is evaluated.
+  for (int64_t q = q0 + lane; q < q1; q += 2 * kWave) {
+    const int64_t qb[2] = {q, q + kWave < q1 ? q + kWave : q};
+    const bool live1 = q + kWave < q1;
+    double d[2][D], x1[2][S1];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) d[u][k] = __builtin_nontemporal_load(g.sdata + qb[u] * D + k);
+      const double* p1 = g.state + g.state_base1 + (int64_t)S1 * g.sid1[qb[u]];
+#pragma unroll
+      for (int k = 0; k < S1; ++k) x1[u][k] = p1[k];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      double r[NR], J0[NR * S0], J1[NR * S1p];
+      if constexpr (kFrame)
+        frame.Evaluate(d[u], x1[u], r, J0);
+      else
+        EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
+#pragma unroll
+      for (int k = 0; k < NR * S1p; ++k) J1[k] = 0.0;
+      LossAndCorrect<K, kLoss, true>(g.loss, g.apply_loss, r, J0, J1);
+      if (u == 0 || live1) {
+#pragma unroll
+        for (int c = 0; c < S0; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < NR; ++k) s += J0[k * S0 + c] * r[k];
+          acc[c] += s;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < S0; ++c)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off, kWave);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < S0; ++c) g.partial[cid * S0 + c] = acc[c];
+  }
+}
+
+// The slot-0-sorted copies CameraGradientKernel streams: functor data and
+// slot-1 ids of block perm[q] at position q.  Once per evaluator.
+template <int D>
+__global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsKernel(const int32_t* ids,
+                                                                       const double* data,
+                                                                       const int32_t* perm,
+                                                                       int64_t n, double* sdata,
+                                                                       int32_t* sid1) {
+  const int64_t q = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (q >= n) return;
+  const int64_t b = perm[q];
+#pragma unroll
+  for (int k = 0; k < D; ++k) sdata[q * D + k] = data[b * D + k];
+  sid1[q] = ids[2 * b + 1];
 }
 
 // The general (table) path for any kind, any number of parameter blocks;

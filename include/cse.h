@@ -167,11 +167,14 @@ typedef struct cse_options {
                                    an evaluator-owned stream */
   int32_t gradient_mode;        /* how g = J^T r is summed when the residuals and
                                    Jacobian are requested too: 0 (default) = fused
-                                   into the evaluation where eligible, else 1;
-                                   1 = a fixed-order post-pass over the written
-                                   Jacobian; 2 = in-kernel FP64 atomics, as
-                                   cuda_evaluator_kernel.h:149-160.  0 and 1 are
-                                   bit-deterministic. */
+                                   where eligible (slot-1 rows in the evaluation,
+                                   slot-0 rows by re-evaluation in slot-0 order),
+                                   else 1; 1 = a fixed-order post-pass over the
+                                   written Jacobian; 2 = in-kernel FP64 atomics,
+                                   as cuda_evaluator_kernel.h:149-160; 3 = fused,
+                                   slot-0 contributions written in block order and
+                                   summed per block (the round-2 form), else 1.
+                                   0, 1 and 3 are bit-deterministic. */
 } cse_options;
 
 typedef struct cse_evaluator cse_evaluator;

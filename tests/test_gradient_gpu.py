@@ -3,10 +3,13 @@ cse_options.gradient_mode), against the CPU oracle's ProgramEvaluator
 gradient (program_evaluator.h:134-290; the reference GPU kernel adds it with
 atomics, cuda_evaluator_kernel.h:149-160):
   0  fused into the evaluation (cse::FusedGrad): slot-1 runs reduced in the
-     wave, slot-0 per-block contributions summed in camera order;
+     wave, slot-0 rows by re-evaluation in camera order
+     (cse::CameraGradientKernel);
   1  the fixed-order post-pass over the written Jacobian;
-  2  in-kernel FP64 atomics.
-Modes 0 and 1 are bit-deterministic; all three agree with the oracle to the
+  2  in-kernel FP64 atomics;
+  3  fused, slot-0 per-block contributions written in block order and summed
+     in camera order (GradientContribKernel).
+Modes 0, 1 and 3 are bit-deterministic; all three agree with the oracle to the
 reference's tolerance (parity_util).  Cases cover the fused path's wave
 boundaries: points whose runs span several waves, one-run waves, ragged
 last chunks (down to one block), both Jacobian layouts and the losses.
@@ -46,6 +49,12 @@ def check_modes(prog):
     assert info.num_fused_gradient_groups == (0 if np.all(np.diff(cams) >= 0) else 1)
     assert_parity(f0, ref, "fused")
     assert np.array_equal(f0[3], f1[3])  # deterministic
+    (c0, c1), info_c = run(prog, 3, repeat=2)
+    assert info_c.num_fused_gradient_groups == info.num_fused_gradient_groups
+    assert_parity(c0, ref, "fused, contributions")
+    assert np.array_equal(c0[3], c1[3])  # deterministic
+    assert np.array_equal(f0[2], c0[2]) and np.array_equal(f0[4], c0[4]) and f0[1] == c0[1]
+    assert is_approx(f0[3], c0[3], 1e-13)
     (p,), info_p = run(prog, 1)
     assert info_p.num_fused_gradient_groups == 0
     assert_parity(p, ref, "post-pass")
