@@ -409,8 +409,9 @@ def main():
         if not args.gradient:
             leg("gradient", lambda: se.evaluate(residuals=True, jacobian=True, gradient=True),
                 info.bytes_jacobian_eval + 8 * ne, ks,
-                "residuals + Jacobian + gradient J^T r + cost (fused deterministic gradient, "
-                "gradient_mode 0; what TrustRegionMinimizer requests); bytes add 8 per "
+                "residuals + Jacobian + gradient J^T r + cost (deterministic gradient_mode 0: "
+                "point rows fused into the evaluation, camera rows re-evaluated in camera "
+                "order; what TrustRegionMinimizer requests); bytes add 8 per "
                 "effective parameter")
         leg("residual_only", lambda: se.evaluate(residuals=True, jacobian=False, gradient=False),
             info.bytes_residual_eval, ks, "residuals + cost (trust-region candidate evaluation)")
@@ -493,9 +494,10 @@ def main():
                 "algorithmic_bytes_per_launch": tot_bytes / world,
                 "kernel_ms_avg": kernel_ms,
                 "kernel_ms_avg_max_rank": kernel_ms_max,
-                "kernel": f"cse::EvaluateAffineChunks{'Fused' if args.gradient else ''}"
+                "kernel": f"cse::EvaluateAffineChunks"
+                          f"{'FusedPoints' if args.gradient else ('TwoRound' if args.format == 'block_sparse' else '')}"
                           f"<SnavelyKind, {args.loss}, {args.format}> (+ repack"
-                          f"{', gradient tail' if args.gradient else ''})",
+                          f"{', CameraGradientKernel and the gradient tail' if args.gradient else ''})",
                 "per": "GPU (bytes of all ranks / N over the slowest rank's kernel time)",
                 "traffic_source": "profiles/pmc_<config>_<loss>_<format>.json (rocprofv3 "
                                   "FETCH_SIZE/WRITE_SIZE of the same kernel)",

@@ -934,90 +934,11 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
   }
 }
 
-// SnavelyReprojectionError's camera partials with the wave's camera fixed
-// (examples/snavely_reprojection_error.h:58-93).  The rotation is linear in
-// the point, so R and its three angle-axis partials are formed once per
-// wave -- column k is AngleAxisRotatePoint(aa, e_k) on Jet<3> angle-axis
-// seeds, the same Rodrigues forms as the evaluation (§3.1) -- and each
-// block's p = R X + t carries its partials as dR/dw_j X (translation: unit
-// partials); the projection and distortion then run on Jet<9> as in the
-// functor.  Against the full Jet<9> functor per block this removes the
-// per-lane Rodrigues evaluation; p differs from the functor's by rounding
-// only (R X summed as a matrix product).
-struct SnavelyCameraFrame {
-  double R[3][3];      // R[i][k]
-  double dR[3][3][3];  // dR[j][i][k] = d R[i][k] / d aa_j
-  double t[3], f, l[2];
-
-  __device__ __forceinline__ void Init(const double* cam) {
-    Jet<3> aa[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) aa[j] = Jet<3>(cam[j], j);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      Jet<3> e[3], col[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) e[i] = Jet<3>(i == k ? 1.0 : 0.0);
-      AngleAxisRotatePoint(aa, e, col);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        R[i][k] = col[i].a;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) dR[j][i][k] = col[i].v[j];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) t[i] = cam[3 + i];
-    f = cam[6];
-    l[0] = cam[7];
-    l[1] = cam[8];
-    // Wave-uniform: held in SGPRs (operands of the per-block FMAs), not in
-    // 84 VGPRs.
-    double* all = &R[0][0];
-    static_assert(sizeof(SnavelyCameraFrame) == 42 * sizeof(double), "frame layout");
-#pragma unroll
-    for (int k = 0; k < 42; ++k) all[k] = Uniform(all[k]);
-  }
-  static __device__ __forceinline__ double Uniform(double x) {
-    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(x));
-    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(x));
-    return __hiloint2double(hi, lo);
-  }
-
-  // r (2) and J0 (2 x 9, row-major) of the block observing X.
-  __device__ __forceinline__ void Evaluate(const double* obs, const double* X, double* r,
-                                           double* J0) const {
-    Jet<9> p[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      p[i] = Jet<9>(R[i][0] * X[0] + R[i][1] * X[1] + R[i][2] * X[2] + t[i]);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) p[i].v[j] = dR[j][i][0] * X[0] + dR[j][i][1] * X[1] + dR[j][i][2] * X[2];
-      p[i].v[3 + i] = 1.0;
-    }
-    const Jet<9> focal(f, 6);
-    const Jet<9> dist[2] = {Jet<9>(l[0], 7), Jet<9>(l[1], 8)};
-    Jet<9> out[2];
-    Project<true>(p, focal, dist, obs, out);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      r[k] = out[k].a;
-#pragma unroll
-      for (int c = 0; c < 9; ++c) J0[k * 9 + c] = out[k].v[c];
-    }
-  }
-};
-
-#ifndef CSE_CAMGRAD_ROTMAT
-#define CSE_CAMGRAD_ROTMAT 0
-#endif
-
 template <class K, int kLoss>
 __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamGradArgs g) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, D = Tr::D;
   static_assert(Tr::NB == 2 && S1 > 0, "two-slot kinds");
-  constexpr bool kFrame = CSE_CAMGRAD_ROTMAT && std::is_same<K, SnavelyKind>::value;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
@@ -1027,8 +948,6 @@ __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamG
   double x0[S0];
 #pragma unroll
   for (int k = 0; k < S0; ++k) x0[k] = cam[k];
-  SnavelyCameraFrame frame;
-  if constexpr (kFrame) frame.Init(x0);
   double acc[S0];
 #pragma unroll
   for (int c = 0; c < S0; ++c) acc[c] = 0.0;
@@ -1049,10 +968,7 @@ __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamG
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       double r[NR], J0[NR * S0], J1[NR * S1p];
-      if constexpr (kFrame)
-        frame.Evaluate(d[u], x1[u], r, J0);
-      else
-        EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
+      EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
 #pragma unroll
       for (int k = 0; k < NR * S1p; ++k) J1[k] = 0.0;
       LossAndCorrect<K, kLoss, true>(g.loss, g.apply_loss, r, J0, J1);
