@@ -62,7 +62,19 @@ def test_rotation_forms_match_the_oracle(gpu, kind, fmt):
     # No loss, so r = predicted - observed and its cancellation can be
     # accounted for (the golden-vector tests' convention): the residuals are
     # held to 1e-13 |predicted| norm-wise plus the per-element bound.
-    prog, obs = _problem(_angles(kind, 3), 3, None, fmt, with_obs=True)
+    angles = _angles(kind, 3)
+    prog, obs = _problem(angles, 3, None, fmt, with_obs=True)
+    # Gradient rows of cameras with 0 < theta < 1e-3.  The fused gradient
+    # (gradient_mode 0) re-evaluates each camera's blocks in waves of that
+    # camera alone, so a tiny-angle camera takes the series form there, while
+    # the oracle (and the point-ordered evaluation, whose waves mix cameras)
+    # follows the reference's form, which loses the Jacobian below 1e-6
+    # (deviation 5).  Those rows are held to 1e-7 relative
+    # here; test_tiny_angles_against_exact_values pins the series form.
+    tiny_cams = np.flatnonzero((angles > 0) & (angles < 1e-3))
+    tiny = np.zeros(prog.num_effective_parameters, bool)
+    for c in tiny_cams:
+        tiny[3 * P + 9 * c: 3 * P + 9 * (c + 1)] = True
     op = O.OracleProgram.from_program(prog, apply_loss_function=True)
     ref = op.evaluate(prog.state, None, num_threads=8)
     for general in (False, True):
@@ -85,6 +97,11 @@ def test_rotation_forms_match_the_oracle(gpu, kind, fmt):
         assert np.linalg.norm(r - ref[2]) <= TOL * pred, (kind, fmt, general)
         assert elementwise_report(r, ref[2])["bound_ratio"] <= 1.0, (kind, fmt, general)
         g_ref = ref[3]
+        if tiny.any():
+            gt, gt_ref = g[tiny], g_ref[tiny]
+            assert np.linalg.norm(gt - gt_ref) <= 1e-7 * np.linalg.norm(gt_ref), \
+                (kind, fmt, general, np.linalg.norm(gt - gt_ref) / np.linalg.norm(gt_ref))
+            g, g_ref = g[~tiny], g_ref[~tiny]
         assert np.linalg.norm(g - g_ref) <= TOL * np.linalg.norm(ref[4]) * np.linalg.norm(ref[2]), \
             (kind, fmt, general, np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref))
         assert elementwise_report(g, g_ref)["bound_ratio"] <= 1.0, (kind, fmt, general)
