@@ -951,14 +951,21 @@ __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamG
   double acc[S0];
 #pragma unroll
   for (int c = 0; c < S0; ++c) acc[c] = 0.0;
-  // Two blocks per lane and step: both blocks' loads are in flight before
-  // either is evaluated.
-  for (int64_t q = q0 + lane; q < q1; q += 2 * kWave) {
-    const int64_t qb[2] = {q, q + kWave < q1 ? q + kWave : q};
-    const bool live1 = q + kWave < q1;
-    double d[2][D], x1[2][S1];
+  // kU blocks per lane and step: their loads are all in flight before the
+  // first is evaluated.  (1, 2 and 4 measured alike, profiles/round2/s5i:
+  // the kernel is insensitive to its occupancy, 2 to 4 waves per SIMD.)
+  constexpr int kU = 2;
+  for (int64_t q = q0 + lane; q < q1; q += kU * kWave) {
+    int64_t qb[kU];
+    bool live[kU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kU; ++u) {
+      live[u] = q + u * kWave < q1;
+      qb[u] = live[u] ? q + u * kWave : q;
+    }
+    double d[kU][D], x1[kU][S1];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int k = 0; k < D; ++k) d[u][k] = __builtin_nontemporal_load(g.sdata + qb[u] * D + k);
       const double* p1 = g.state + g.state_base1 + (int64_t)S1 * g.sid1[qb[u]];
@@ -966,13 +973,13 @@ __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamG
       for (int k = 0; k < S1; ++k) x1[u][k] = p1[k];
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kU; ++u) {
       double r[NR], J0[NR * S0], J1[NR * S1p];
       EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
 #pragma unroll
       for (int k = 0; k < NR * S1p; ++k) J1[k] = 0.0;
       LossAndCorrect<K, kLoss, true>(g.loss, g.apply_loss, r, J0, J1);
-      if (u == 0 || live1) {
+      if (live[u]) {
 #pragma unroll
         for (int c = 0; c < S0; ++c) {
           double s = 0.0;
