@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--lib", default=None, help="tuning library to load (default lib/libcse_tuning.so)")
     ap.add_argument("--mode", default="jacobian", choices=["jacobian", "gradient", "residual", "cost"])
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="time rank 0's shard of an N-way point-bucket cut instead")
     args = ap.parse_args()
     import torch
     # "26s16": variant 26 with the slot-0 table repacked at a 16-double stride
@@ -49,7 +51,12 @@ def main():
     variants = args.variants.split(",")
     loss = {"huber": ca.Loss.huber(1.0), "trivial": ca.Loss.trivial()}[args.loss]
     t0 = time.time()
-    prog = bal.synthetic_program(args.config, loss=loss)
+    if args.shard_of > 1:
+        from ceres_amd import shard
+        prog = shard.shard_program(*bal.synthetic(*bal.CONFIGS[args.config]), 0, args.shard_of,
+                                   loss=loss)[0]
+    else:
+        prog = bal.synthetic_program(args.config, loss=loss)
     print(f"# built {args.config} in {time.time() - t0:.1f} s", flush=True)
     dev = torch.device("cuda", 0)
     f64 = torch.float64
@@ -61,6 +68,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ref_hash = None
     times = {v: [] for v in variants}
+    walls = {v: [] for v in variants}  # wall ms per evaluation (every launch)
     bytes_ = None
     for rnd in range(args.rounds):
         for v in variants:
@@ -95,9 +103,13 @@ def main():
                 same = digest == ref_hash
                 print(f"# variant {v}: outputs {'identical' if same else 'DIFFER'}", flush=True)
             ev.reset_kernel_stats()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             for _ in range(args.steps):
                 ev.evaluate_device(state.data_ptr(), cost.data_ptr(), rp, gp, jp)
             assert ev.wait() == 0
+            torch.cuda.synchronize()
+            walls[v].append((time.perf_counter() - t0) / args.steps * 1e3)
             _, total, n = ev.kernel_stats()
             ev.close()
             ms = total / n
@@ -105,6 +117,7 @@ def main():
             print(f"round {rnd} variant {v}: {ms:.4f} ms  {bytes_ / ms / 1e6:.0f} GB/s  "
                   f"frac {bytes_ / ms / 1e6 / 8000:.3f}", flush=True)
     summary = {v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                   "median_wall_ms": float(np.median(walls[v])),
                    "frac_median": bytes_ / float(np.median(t)) / 1e6 / 8000} for v, t in times.items()}
     print(json.dumps({"mode": args.mode, "summary": summary}))
     if args.out:

@@ -14,8 +14,8 @@ for r in $(seq 1 $ROUNDS); do
       lib=$L/libcse.so
       [ $which != base ] && lib=$L/$which/libcse.so
       timeout -k 10 200 python -u tools/ab_bench.py --lib $lib --variants 0 --rounds 2 --steps 20 \
-        --mode $m > $OUT/ab_${m}_${which}_$r.txt 2>&1 || { echo "ab rc=$? ($m $which)"; tail -5 $OUT/ab_${m}_${which}_$r.txt; exit 1; }
-      echo "$m $which r$r: $(tail -1 $OUT/ab_${m}_${which}_$r.txt | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["summary"]["0"]["median_ms"])')"
+        --mode $m $AB_ARGS > $OUT/ab_${m}_${which}_$r.txt 2>&1 || { echo "ab rc=$? ($m $which)"; tail -5 $OUT/ab_${m}_${which}_$r.txt; exit 1; }
+      echo "$m $which r$r: $(tail -1 $OUT/ab_${m}_${which}_$r.txt | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["summary"]["0"]["median_ms"], "wall", d["summary"]["0"]["median_wall_ms"])')"
     done
   done
 done
