@@ -216,6 +216,14 @@ void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
+// The shipped CRS Jacobian kernel (two half-wave staging rounds, 4 waves
+// per SIMD).
+template <class K, int L, int Co>
+void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrs<K, L, Co>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
+}
+
 // The affine kernel with the fused gradient (Snavely groups): with the
 // slot-0 contributions (gradient_mode 3) or points only (gradient_mode 0,
 // slot 0 from CameraGradientKernel).
@@ -254,6 +262,10 @@ LaunchFn PickAffine(bool jac, bool dma) {
   if constexpr (!Crs && cse::kTwoRoundBsm<K>) {
     // (the 8-byte-piece gather of kCoop 1 would spill at 128 VGPRs)
     if (jac && dma) return &LaunchTwoRound<K, L, 2>;
+  }
+  if constexpr (Crs) {
+    // 1778 CRS 0.298 -> 0.285 ms, 13682 CRS 1.540 -> 1.480 ms (profiles/round2/s5k)
+    if (jac && dma) return &LaunchTwoRoundCrs<K, L, 2>;
   }
   if (dma) return jac ? &LaunchChunks<K, L, true, Crs, 2> : &LaunchChunks<K, L, false, Crs, 2>;
   return jac ? &LaunchChunks<K, L, true, Crs, 1> : &LaunchChunks<K, L, false, Crs, 1>;

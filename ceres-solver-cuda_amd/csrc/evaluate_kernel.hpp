@@ -34,7 +34,9 @@ namespace cse {
 //       [jac_base[j][0] + stride_j*i0, + kR*size_j*nw)
 //   kCrs = true (CompressedRowSparseMatrix): whole blocks, kR rows of N
 //       columns, at [row0 + kR*N*i0, + kR*N*nw)
-template <class K, bool kJac, bool kCrs>
+//   kHalves (CRS): the rows staged and written for lanes [0, 32), then for
+//       lanes [32, 64), through half the LDS.
+template <class K, bool kJac, bool kCrs, bool kHalves = false>
 __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
                                               int64_t i0, int nw, const double* r,
                                               const double* J0, const double* J1) {
@@ -52,22 +54,31 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
     if constexpr (kCrs) {
       const int64_t row0 = a.jac_base[0][0] < a.jac_base[NB - 1][0] ? a.jac_base[0][0]
                                                                       : a.jac_base[NB - 1][0];
-      if (active) {
+      constexpr int kParts = kHalves ? 2 : 1, kLanes = kWave / kParts;
 #pragma unroll
-        for (int k = 0; k < NR; ++k) {
-          const int c0 = (int)(a.jac_base[0][k] - row0);
+      for (int h = 0; h < kParts; ++h) {
+        const int lo = h * kLanes;
+        const int cnt = nw - lo < kLanes ? nw - lo : kLanes;
+        if (cnt <= 0) break;
+        if (active && lane >= lo && lane < lo + kLanes) {
+          double* row = st + (lane - lo) * NR * N;
 #pragma unroll
-          for (int c = 0; c < S0; ++c) st[lane * NR * N + c0 + c] = J0[k * S0 + c];
-          if constexpr (S1 > 0) {
-            const int c1 = (int)(a.jac_base[1][k] - row0);
+          for (int k = 0; k < NR; ++k) {
+            const int c0 = (int)(a.jac_base[0][k] - row0);
 #pragma unroll
-            for (int c = 0; c < S1; ++c) st[lane * NR * N + c1 + c] = J1[k * S1p + c];
+            for (int c = 0; c < S0; ++c) row[c0 + c] = J0[k * S0 + c];
+            if constexpr (S1 > 0) {
+              const int c1 = (int)(a.jac_base[1][k] - row0);
+#pragma unroll
+              for (int c = 0; c < S1; ++c) row[c1 + c] = J1[k * S1p + c];
+            }
           }
         }
+        __builtin_amdgcn_wave_barrier();
+        WaveStore(st, a.jacobian + row0 + (int64_t)NR * N * (i0 + lo), cnt * NR * N, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
-      WaveStore(st, a.jacobian + row0 + (int64_t)NR * N * i0, nw * NR * N, lane);
-      __builtin_amdgcn_wave_barrier();
     } else {
       // Two rounds through the same LDS (slot 0's cells, then slot 1's): the
       // fast tail may size the staging buffer for slot 0 alone.
@@ -428,6 +439,21 @@ __device__ __forceinline__ void ReadSegmentPieces(const double* staged, int hp, 
   const double2 v = st2[LastPiece<kQ, kA>(lane, hp)];
   q[kQ - 1] = AsV4i(v.x, v.y);
 }
+// The same for a segment staged in parts: only the pieces in [lo, hi) are
+// read, from staged + 16 * (piece - lo) bytes (the others keep their value).
+template <int kQ, int kA = 64>
+__device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int hp, int lane,
+                                                       int lo, int hi, cse_v4i* q) {
+  const double2* st2 = reinterpret_cast<const double2*>(staged);
+#pragma unroll
+  for (int j = 0; j < kQ; ++j) {
+    const int p = j < kQ - 1 ? j * kWave + lane + hp : LastPiece<kQ, kA>(lane, hp);
+    if (p >= lo && p < hi) {
+      const double2 v = st2[p - lo];
+      q[j] = AsV4i(v.x, v.y);
+    }
+  }
+}
 
 // Compile-time knobs of the affine kernel.  The product instantiates only
 // ShippedTune; other settings exist in the tuning build (-DCSE_TUNING,
@@ -508,15 +534,17 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   static_assert(!MayLeaveOutputs<K>::value, "affine kernels: functors that assign every output");
   constexpr bool kLdsE = T::kLdsE || kCrs || !kJac;
   constexpr bool kTwo = T::kTwoRound && kJac && !kCrs && kLdsE && S1 > 0;
+  // CRS rows staged in two halves of the wave (lanes [0, 32), then [32, 64)).
+  constexpr bool kTwoCrs = T::kTwoRound && kJac && kCrs;
   constexpr int kA = T::kAlign;
-  constexpr int kOutLane = kJac ? (kCrs ? NR * N
+  constexpr int kOutLane = kJac ? (kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N)
                                         : kTwo ? NR * (S0 > S1 ? S0 : S1)
                                                : kLdsE ? NR * (S0 + S1) : NR * S0)
                                 : 1;
   constexpr int kCoopLane = kCoop == 2 ? ((S0 + 1) & ~1) : S0;
   // StageAndStore's footprint (ragged chunks): whole rows (CRS) or one
   // slot's cells at a time (BSM).
-  constexpr int kSlowLane = !kJac ? 1 : kCrs ? NR * N : NR * (S0 > S1 ? S0 : S1);
+  constexpr int kSlowLane = !kJac ? 1 : kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N) : NR * (S0 > S1 ? S0 : S1);
   constexpr int kStageLane0 = kCoopLane > kOutLane ? kCoopLane : kOutLane;
   constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
   constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
@@ -606,7 +634,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
   if (!FastTail<K, kJac, kCrs>(a, i0, nw)) {
-    StageAndStore<K, kJac, kCrs>(a, st, lane, active, i0, nw, r, J0, J1);
+    StageAndStore<K, kJac, kCrs, kTwoCrs>(a, st, lane, active, i0, nw, r, J0, J1);
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;
@@ -653,18 +681,39 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         const int64_t row0 = a.jac_base[0][0] < a.jac_base[Tr::NB - 1][0]
                                  ? a.jac_base[0][0]
                                  : a.jac_base[Tr::NB - 1][0];
+        // Lane `lane`'s row block at `row` (kTwoCrs: the half-wave's rows).
+        auto stage_rows = [&](double* row) {
 #pragma unroll
-        for (int k = 0; k < NR; ++k) {
-          const int c0 = (int)(a.jac_base[0][k] - row0);
+          for (int k = 0; k < NR; ++k) {
+            const int c0 = (int)(a.jac_base[0][k] - row0);
 #pragma unroll
-          for (int cc = 0; cc < S0; ++cc) st[lane * NR * N + c0 + cc] = J0[k * S0 + cc];
-          if constexpr (S1 > 0) {
-            const int c1 = (int)(a.jac_base[1][k] - row0);
+            for (int cc = 0; cc < S0; ++cc) row[c0 + cc] = J0[k * S0 + cc];
+            if constexpr (S1 > 0) {
+              const int c1 = (int)(a.jac_base[1][k] - row0);
 #pragma unroll
-            for (int cc = 0; cc < S1; ++cc) st[lane * NR * N + c1 + cc] = J1[k * S1p + cc];
+              for (int cc = 0; cc < S1; ++cc) row[c1 + cc] = J1[k * S1p + cc];
+            }
           }
-        }
+        };
         seg0 = a.jacobian + row0 + (int64_t)NR * N * i0;
+        if constexpr (kTwoCrs) {
+          // Lanes [0, 32) stage their rows (the segment's first half), every
+          // lane reads the pieces that fall in it; then lanes [32, 64) and
+          // the second half, in the same LDS.  FastTail guarantees NR * N
+          // even, so the halves split on a piece boundary.
+          constexpr int kHalf = kWave / 2 * NR * N / 2;  // pieces per half
+          hp0 = SectorHeadPieces<kA>(seg0);
+          if (lane < kWave / 2) stage_rows(st + lane * NR * N);
+          __builtin_amdgcn_wave_barrier();
+          ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, 0, kHalf, q0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          if (lane >= kWave / 2) stage_rows(st + (lane - kWave / 2) * NR * N);
+          __builtin_amdgcn_wave_barrier();
+          ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, kHalf, 2 * kHalf, q0);
+        } else {
+          stage_rows(st + lane * NR * N);
+        }
       } else {
         double* st1 = st + kWave * NR * S0;
 #pragma unroll
@@ -680,9 +729,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         }
         seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
       }
-      __builtin_amdgcn_wave_barrier();
-      hp0 = SectorHeadPieces<kA>(seg0);
-      ReadSegmentPieces<kQ0, kA>(st, hp0, lane, q0);
+      if constexpr (!kTwoCrs) {
+        __builtin_amdgcn_wave_barrier();
+        hp0 = SectorHeadPieces<kA>(seg0);
+        ReadSegmentPieces<kQ0, kA>(st, hp0, lane, q0);
+      }
       if constexpr (kQ1 > 0) {
         hp1 = SectorHeadPieces<kA>(seg1);
         if constexpr (kTwo) {
@@ -852,6 +903,14 @@ template <class K, int kLoss, int kCoop>
 __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound(const GroupArgs a) {
   static_assert(kTwoRoundBsm<K>, "two-slot kinds");
   AffineChunkBody<K, kLoss, true, false, kCoop, false, ShippedTune>(a);
+}
+
+// The shipped CRS Jacobian kernel: rows staged in two half-waves (24 KiB of
+// LDS a workgroup) and held to 4 waves per SIMD (128 VGPRs), as the BSM
+// kernel; one-round staging took 48 KiB and 130 VGPRs (3 waves per SIMD).
+template <class K, int kLoss, int kCoop>
+__global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRoundCrs(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, true, true, kCoop, false, ShippedTune>(a);
 }
 
 // The same held to at least kMinWaves waves per SIMD (a register bound:

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--lib", default=None, help="tuning library to load (default lib/libcse_tuning.so)")
     ap.add_argument("--mode", default="jacobian", choices=["jacobian", "gradient", "residual", "cost"])
+    ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
     ap.add_argument("--shard-of", type=int, default=0,
                     help="time rank 0's shard of an N-way point-bucket cut instead")
     args = ap.parse_args()
@@ -54,9 +55,9 @@ def main():
     if args.shard_of > 1:
         from ceres_amd import shard
         prog = shard.shard_program(*bal.synthetic(*bal.CONFIGS[args.config]), 0, args.shard_of,
-                                   loss=loss)[0]
+                                   loss=loss, format=args.format)[0]
     else:
-        prog = bal.synthetic_program(args.config, loss=loss)
+        prog = bal.synthetic_program(args.config, loss=loss, format=args.format)
     print(f"# built {args.config} in {time.time() - t0:.1f} s", flush=True)
     dev = torch.device("cuda", 0)
     f64 = torch.float64
