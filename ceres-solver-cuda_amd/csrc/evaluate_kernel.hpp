@@ -932,10 +932,11 @@ EvaluateAffineChunksFused(const GroupArgs a) {
 
 // The fused gradient's points-only form: the slot-1 rows and boundary
 // entries as above, no slot-0 contributions (CameraGradientKernel computes
-// the slot-0 sums).  Without the contribution registers the BSM form fits
-// 128 VGPRs, so it runs at the two-round kernel's 4 waves per SIMD.
+// the slot-0 sums).  Without the contribution registers both forms fit 128
+// VGPRs and run at 4 waves per SIMD (CRS with the half-wave staging: 2.33 ->
+// 2.25 ms against 3 waves, profiles/round2/s5l).
 template <class K, int kLoss, bool kCrs>
-__global__ __launch_bounds__(kBlockThreads, kCrs ? 3 : 4) void EvaluateAffineChunksFusedPoints(
+__global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksFusedPoints(
     const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, kCrs, 2, true, PointsOnlyTune>(a);
 }
