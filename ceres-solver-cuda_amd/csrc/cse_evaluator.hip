@@ -183,6 +183,7 @@ struct Group {
   // on first use).
   DevBuf<double> sdata;
   DevBuf<int32_t> sid1;
+  bool sorted_ready = false;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -733,15 +734,16 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
   const Group::GradPlan& P = G.grad[0];
   const int D = G.shape.data;
   int rc;
-  if (G.sdata.p == nullptr) {
+  if (!G.sorted_ready) {  // set only once the copies have been queued
+    if (D != 2) return Fail(CSE_ERR_UNSUPPORTED, "camera-order gradient: 2 data doubles per block");
     if ((rc = G.sdata.alloc((size_t)G.n * D))) return rc;
     if ((rc = G.sid1.alloc((size_t)G.n))) return rc;
-    if (D != 2) return Fail(CSE_ERR_UNSUPPORTED, "camera-order gradient: 2 data doubles per block");
     hipLaunchKernelGGL((cse::SortSlot0InputsKernel<2>),
                        dim3((unsigned)((G.n + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                        dim3(cse::kBlockThreads), 0, s, G.ids.p, G.data.p, P.perm.p, G.n, G.sdata.p,
                        G.sid1.p);
     CSE_HIP(hipGetLastError());
+    G.sorted_ready = true;
   }
   const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
   hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
