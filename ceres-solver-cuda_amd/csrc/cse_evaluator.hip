@@ -337,6 +337,11 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 28: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16, true>>;
     case 29: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 4>>;
     case 30: return &LaunchChunks<K, L, true, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 5>>;
+    // E-cell / residual store policies on the shipped two-round kernel
+    case 31: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 1, 0>, 4>;
+    case 32: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 2, 0>, 4>;
+    case 33: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 1, 1>, 4>;
+    case 34: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 1>, 4>;
     default: return nullptr;
   }
 }

@@ -485,9 +485,12 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
 //   kDmaOwn  LDS-DMA of each lane's own row (GatherCoopDma kOwn).
 //   kNoContrib  fused gradient without the slot-0 contributions (the slot-0
 //           sums come from CameraGradientKernel instead).
+//   kEPol, kRPol  cache policy (StoreNt16 kPol) of the E-cell and residual
+//           stores (the F cells keep nt sc1).
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
-          int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false>
+          int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
+          int kEPol_ = 0, int kRPol_ = 0>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -501,6 +504,8 @@ struct Tune {
   static constexpr int kCamStride = kCamStride_;
   static constexpr bool kDmaOwn = kDmaOwn_;
   static constexpr bool kNoContrib = kNoContrib_;
+  static constexpr int kEPol = kEPol_;  // StoreNt16 policy of the E-cell stores
+  static constexpr int kRPol = kRPol_;  // and of the residual stores
 };
 // Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
 // sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
@@ -830,8 +835,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kQ1 > 0) {
       if (!jac) return;
       if constexpr (kLdsE) {
-        SegmentStoresFrom<0, kQ1 - 1>(e0, e1, q1);
-        StoreNt16<0>(elast, q1[kQ1 - 1]);
+        SegmentStoresFrom<0, kQ1 - 1, T::kEPol>(e0, e1, q1);
+        StoreNt16<0, T::kEPol>(elast, q1[kQ1 - 1]);
       } else {
         // Per-lane pieces at a 48-byte lane stride: each instruction covers
         // a third of every line of the segment, default policy so that the
@@ -845,9 +850,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   };
   auto store_r = [&]() {
     if (a.residuals) {  // a kernel argument: a scalar branch, no VALU after the stores
-      if constexpr (kQr >= 1) StoreNt16<0>(rdst, qr[0]);
-      if constexpr (kQr >= 2) StoreNt16<16>(rdst, qr[1]);
-      if constexpr (kQr >= 3) StoreNt16<32>(rdst, qr[2]);
+      if constexpr (kQr >= 1) StoreNt16<0, T::kRPol>(rdst, qr[0]);
+      if constexpr (kQr >= 2) StoreNt16<16, T::kRPol>(rdst, qr[1]);
+      if constexpr (kQr >= 3) StoreNt16<32, T::kRPol>(rdst, qr[2]);
     }
   };
   if constexpr (T::kOrder == 1) {
