@@ -342,6 +342,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 32: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 2, 0>, 4>;
     case 33: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 1, 1>, 4>;
     case 34: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 1>, 4>;
+    case 35: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 3, 3, 3>, 4>;
+    case 36: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 4, 4, 4>, 4>;
     default: return nullptr;
   }
 }

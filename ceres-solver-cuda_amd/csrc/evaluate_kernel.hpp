@@ -490,7 +490,7 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
           int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
-          int kEPol_ = 0, int kRPol_ = 0>
+          int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -506,6 +506,7 @@ struct Tune {
   static constexpr bool kNoContrib = kNoContrib_;
   static constexpr int kEPol = kEPol_;  // StoreNt16 policy of the E-cell stores
   static constexpr int kRPol = kRPol_;  // and of the residual stores
+  static constexpr int kFPol = kFPol_;  // and of the F-cell stores
 };
 // Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
 // sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
@@ -826,8 +827,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   auto store_f = [&]() {
     if constexpr (T::kDiag == 4) return;
     if (jac) {
-      SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0)>(f0, f1, q0);
-      if constexpr (kQ0 > 0) StoreNt16<0>(flast, q0[kQ0 - 1]);
+      SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0), T::kFPol>(f0, f1, q0);
+      if constexpr (kQ0 > 0) StoreNt16<0, T::kFPol>(flast, q0[kQ0 - 1]);
     }
   };
   auto store_e = [&]() {

@@ -336,7 +336,7 @@ __device__ __forceinline__ cse_v4i AsV4i(double a, double b) {
 // 16-byte store at base + kOff bytes (kOff in [-4096, 4095]).  kPol: the
 // cache policy, 0 = nt sc1 (streaming, not kept in the XCD's L2; 6-8 %
 // faster than nt alone on the evaluator's output stream, profiles/r02),
-// 1 = default policy, 2 = nt.
+// 1 = default policy, 2 = nt, 3 = sc0 sc1 nt, 4 = sc0 sc1 (tuning only).
 template <int kOff, int kPol = 0>
 __device__ __forceinline__ void StoreNt16(double* base, const cse_v4i& d) {
   static_assert(kOff >= -4096 && kOff <= 4095, "global offset out of range");
@@ -345,6 +345,13 @@ __device__ __forceinline__ void StoreNt16(double* base, const cse_v4i& d) {
                  : "memory");
   else if constexpr (kPol == 2)
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2 nt" ::"v"(base), "v"(d), "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 3)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1 nt" ::"v"(base), "v"(d),
+                 "i"(kOff)
+                 : "memory");
+  else if constexpr (kPol == 4)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1" ::"v"(base), "v"(d), "i"(kOff)
                  : "memory");
   else
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1 nt" ::"v"(base), "v"(d),
