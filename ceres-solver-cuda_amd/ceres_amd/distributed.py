@@ -92,21 +92,28 @@ class ShardedEvaluator:
                                        ptr(self.gradient, gradient),
                                        ptr(self.jacobian, jacobian))
         if self.exchange:
-            if overlap and not self._host_reduce:
-                self._pending.append(self.dist.all_reduce(cost, group=self.group, async_op=True))
-            else:
-                self._all_reduce(cost)
-            if gradient:
-                lo, hi = self._cam_rows
-                self._all_reduce(self.gradient[lo:hi])
+            # The collectives are ordered against the evaluation's stream: a
+            # collective (and gloo's host copy) follows torch's current
+            # stream, so it is issued with self.stream current.
+            with self.torch.cuda.stream(self.stream):
+                if overlap and not self._host_reduce:
+                    self._pending.append(self.dist.all_reduce(cost, group=self.group,
+                                                              async_op=True))
+                else:
+                    self._all_reduce(cost)
+                if gradient:
+                    lo, hi = self._cam_rows
+                    self._all_reduce(self.gradient[lo:hi])
 
     def wait_exchange(self):
         """Order every overlapped all-reduce before later work on the stream."""
-        for w in self._pending:
-            w.wait()
+        with self.torch.cuda.stream(self.stream):
+            for w in self._pending:
+                w.wait()
         self._pending = []
 
     def _all_reduce(self, t):
+        """All-reduce t (sum) after the work queued on self.stream."""
         if self._host_reduce:
             h = t.cpu()
             self.dist.all_reduce(h, group=self.group)

@@ -29,13 +29,16 @@ def point_bucket_cuts(pt_idx, num_points, world, align=4, search=64):
     point-major (nondecreasing).  Returns (point_cuts, block_cuts), each of
     length world + 1.
 
-    Each cut is moved to the first point boundary at or after its target
-    whose block index is a multiple of `align` (looking at most `search`
-    boundaries ahead; else the plain boundary).  With align = 4 every
-    rank's block count is a multiple of 4, so its rank-local
+    Each cut goes to the first point boundary at or after its target.  It
+    is then moved on to the next boundary whose block index is a multiple of
+    `align` (looking at most `search` boundaries ahead), but only while that
+    stays below the next rank's target, so that alignment never empties or
+    overruns a rank; otherwise the plain boundary stays.  With align = 4 every
+    rank's block count is then a multiple of 4, so its rank-local
     BlockSparseMatrix F cells (at 6 * blocks doubles) start on a 64-byte
     sector and the evaluator's store windows need no partial sectors
-    (DESIGN.md §4.3)."""
+    (DESIGN.md §4.3).  Ranks can be empty only when there are fewer points
+    than ranks."""
     pt_idx = np.asarray(pt_idx)
     if pt_idx.size and np.any(np.diff(pt_idx) < 0):
         raise ValueError("observations must be point-major (Schur order)")
@@ -45,13 +48,15 @@ def point_bucket_cuts(pt_idx, num_points, world, align=4, search=64):
     pc = [0]
     for r in range(1, world):
         target = O * r // world
+        next_target = O * (r + 1) // world
         p = int(np.searchsorted(csum, target))  # first point whose start >= target
+        p = max(p, pc[-1])
         if align > 1:
             window = csum[p:p + search]
-            hit = np.nonzero(window % align == 0)[0]
+            hit = np.nonzero((window % align == 0) & (window < next_target))[0]
             if hit.size:
                 p += int(hit[0])
-        pc.append(max(p, pc[-1]))
+        pc.append(min(p, int(num_points)))
     pc.append(int(num_points))
     bc = [int(csum[p]) for p in pc]
     return pc, bc

@@ -18,11 +18,15 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
 #include "../../include/cse.h"
 #include "schur_kernels.hpp"
+#ifdef CSE_TUNING
+#include "pipeline_launch.h"
+#endif
 
 namespace {
 
@@ -217,6 +221,23 @@ void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
+#ifdef CSE_TUNING
+// Tuning build: the persistent wave-specialised BSM Jacobian kernel
+// (pipeline.hip; measured slower than the shipped kernel).
+template <class K, int L, int kStoreWaves, int kOpt = 0>
+void LaunchPipelined(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  static_assert(std::is_same<K, cse::SnavelyKind>::value, "Snavely only");
+  (void)num_wg;
+  cse::LaunchPipelinedSnavely<L, kStoreWaves, kOpt>(a, s);
+}
+
+template <class K, int L, int kStoreWaves, int kOpt = 0>
+void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  (void)num_wg;
+  cse::LaunchPipelinedSnavelyProbe<L, kStoreWaves, kOpt>(a, s);
+}
+#endif
+
 // The shipped CRS Jacobian kernel (two half-wave staging rounds, 4 waves
 // per SIMD).
 template <class K, int L, int Co>
@@ -344,6 +365,19 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 34: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 1>, 4>;
     case 35: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 3, 3, 3>, 4>;
     case 36: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 4, 4, 4>, 4>;
+    // persistent wave-specialised pipeline, 4 / 3 / 2 store waves
+    case 40: return &LaunchPipelined<K, L, 4>;
+    case 41: return &LaunchPipelined<K, L, 3>;
+    case 42: return &LaunchPipelined<K, L, 2>;
+    case 43: return &LaunchPipelinedProbe<K, L, 4>;
+    case 44: return &LaunchPipelined<K, L, 6>;
+    case 45: return &LaunchPipelined<K, L, 8>;
+    case 46: return &LaunchPipelinedProbe<K, L, 8>;
+    // ... with the compute waves at s_setprio 3
+    case 47: return &LaunchPipelined<K, L, 8, 2>;
+    case 48: return &LaunchPipelined<K, L, 4, 2>;
+    case 49: return &LaunchPipelined<K, L, 6, 2>;
+    case 50: return &LaunchPipelinedProbe<K, L, 8, 2>;
     default: return nullptr;
   }
 }
@@ -690,6 +724,7 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.loss.scaled = G.loss.scaled;
   a.apply_loss = ev->opts.apply_loss_function;
   a.check_finite = ev->opts.check_finite;
+  a.num_cus = ev->num_cus;
   return a;
 }
 
@@ -1005,6 +1040,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   if (!ev) return Fail(CSE_ERR_OOM, "host allocation failed");
   if (options) ev->opts = *options; else cse_default_options(&ev->opts);
   auto bail = [&](int code) { cse_destroy(ev); return code; };
+  if (ev->opts.gradient_mode < 0 || ev->opts.gradient_mode > 3)
+    return bail(Fail(CSE_ERR_INVALID, "gradient_mode " + std::to_string(ev->opts.gradient_mode) +
+                                          " is not one of 0..3"));
 
   if (ev->opts.device >= 0) {
     if (hipSetDevice(ev->opts.device) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "hipSetDevice failed"));
@@ -1429,6 +1467,7 @@ cse::SchurArgs MakeSchurArgs(cse_evaluator* ev, const double* x, double* y) {
   a.nchunks = S.nchunks;
   a.big = S.big.p;
   a.nbig = S.nbig;
+  a.status = ev->status.p + 1;  // read by cse_wait
   return a;
 }
 
@@ -1507,7 +1546,9 @@ int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const dou
   S.D = d_D;
   S.b = d_b;
   S.preconditioner = preconditioner;
-  // M_p and rhs = F^T (b - E M E^T b).
+  // M_p and rhs = F^T (b - E M E^T b).  The status word read by cse_wait
+  // reports a non-positive pivot (schur_kernels.hpp, PivotOk).
+  CSE_HIP(hipMemsetAsync(ev->status.p + 1, 0, sizeof(int), s));
   CSE_HIP(hipMemsetAsync(d_rhs, 0, S.f_cols * sizeof(double), s));
   cse::SchurArgs a = MakeSchurArgs(ev, nullptr, nullptr);
   LaunchSchurPass<cse::kSchurInit>(a, s);
@@ -1531,7 +1572,7 @@ int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const dou
     // d_off: D index of camera lo + p = e_cols + f index = e_cols + f_col_base + 9 (lo + p).
     hipLaunchKernelGGL((cse::SchurBlockInvertKernel<9>), dim3((unsigned)((P.count + 63) / 64)),
                        dim3(64), 0, s, ch, P.count, d_D,
-                       S.e_cols + S.f_col_base + 9LL * P.lo, S.precond.p);
+                       S.e_cols + S.f_col_base + 9LL * P.lo, S.precond.p, ev->status.p + 1);
     CSE_HIP(hipGetLastError());
   }
   S.ready = true;

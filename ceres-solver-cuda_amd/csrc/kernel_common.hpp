@@ -74,6 +74,8 @@ struct GroupArgs {
   LossParams loss;
   int apply_loss;
   int check_finite;
+  int num_cus;  // compute units of the device (persistent launches)
+  unsigned long long* probe;  // tuning build: per-wave cycle accounting (pipeline kernel)
 };
 
 // Compile-time shape of a functor kind: kR residuals, NB parameter blocks

@@ -53,22 +53,41 @@ struct SchurArgs {
   int64_t nchunks;
   const int64_t* big;      // [nbig][2] runs longer than a wave
   int64_t nbig;
+  int* status;             // set to 1 when a pivot of E^T E + D_e^2 is not positive
 };
+
+// A Cholesky pivot that can be factored: positive and finite.  Bit tests:
+// the kernels are compiled with -ffinite-math-only, which folds NaN checks.
+__device__ __forceinline__ bool PivotOk(double p) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, p);
+  return (b >> 63) == 0 && b != 0 && ((b >> 52) & 0x7ff) != 0x7ff;
+}
 
 // Packed upper triangle of a symmetric 3 x 3: (00, 01, 02, 11, 12, 22).
 // M = (A + diag(d^2))^-1 by the Cholesky factor, as the reference's
 // m.selfadjointView<Upper>().llt().solve(Identity) (implicit_schur_
-// complement.cc:207-211): A = L L^T, M = L^-T L^-1.
-__device__ __forceinline__ void InvertSpd3(const double* A, const double* d, double* M) {
+// complement.cc:207-211): A = L L^T, M = L^-T L^-1.  Returns false (and M =
+// 0) when a pivot is not positive -- A + diag(d^2) singular or indefinite,
+// e.g. a point seen by a single residual block with D = NULL.  Eigen's LLT
+// would return NaN/Inf there; the caller raises the status word instead.
+__device__ __forceinline__ bool InvertSpd3(const double* A, const double* d, double* M) {
   const double a00 = A[0] + d[0] * d[0], a11 = A[3] + d[1] * d[1], a22 = A[5] + d[2] * d[2];
-  const double l00 = sqrt(a00);
+  const double p0 = a00;
+  const double l00 = sqrt(p0);
   const double i00 = 1.0 / l00;
   const double l10 = A[1] * i00, l20 = A[2] * i00;
-  const double l11 = sqrt(a11 - l10 * l10);
+  const double p1 = a11 - l10 * l10;
+  const double l11 = sqrt(p1);
   const double i11 = 1.0 / l11;
   const double l21 = (A[4] - l20 * l10) * i11;
-  const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
+  const double p2 = a22 - l20 * l20 - l21 * l21;
+  const double l22 = sqrt(p2);
   const double i22 = 1.0 / l22;
+  if (!(PivotOk(p0) && PivotOk(p1) && PivotOk(p2))) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) M[k] = 0.0;
+    return false;
+  }
   // L^-1 (lower): rows (i00), (j10 i11), (j20 j21 i22).
   const double j10 = -l10 * i00 * i11;
   const double j21 = -l21 * i11 * i22;
@@ -79,6 +98,7 @@ __device__ __forceinline__ void InvertSpd3(const double* A, const double* d, dou
   M[3] = i11 * i11 + j21 * j21;
   M[4] = j21 * i22;
   M[5] = i22 * i22;
+  return true;
 }
 
 __device__ __forceinline__ void SymMul3(const double* M, const double* s, double* w) {
@@ -264,7 +284,8 @@ __global__ __launch_bounds__(kBlockThreads) void SchurChunkKernel(const SchurArg
 #pragma unroll
       for (int k = 0; k < 3; ++k) d[k] = a.D[ecol + k];
     }
-    InvertSpd3(A, d, M);
+    const bool ok = InvertSpd3(A, d, M);
+    if (active && lane == e && !ok) *a.status = 1;
     if (active && lane == e) {
       double* m = a.ete_inv + 2 * ecol;
 #pragma unroll
@@ -351,7 +372,8 @@ __global__ __launch_bounds__(kBlockThreads) void SchurBigKernel(const SchurArgs 
 #pragma unroll
       for (int k = 0; k < 3; ++k) d[k] = a.D[ecol + k];
     }
-    InvertSpd3(A, d, M);
+    const bool ok = InvertSpd3(A, d, M);
+    if (lane == 0 && !ok) *a.status = 1;
     if (lane == 0) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) a.ete_inv[2 * ecol + k] = M[k];
@@ -481,7 +503,7 @@ __global__ __launch_bounds__(kBlockThreads) void SchurBlockDiagKernel(const Schu
 template <int S0>
 __global__ __launch_bounds__(64) void SchurBlockInvertKernel(const GradChunks ch, int64_t count,
                                                              const double* D, int64_t d_off,
-                                                             double* P) {
+                                                             double* P, int* status) {
   constexpr int T = SymCount<S0>();
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= count) return;
@@ -506,12 +528,16 @@ __global__ __launch_bounds__(64) void SchurBlockInvertKernel(const GradChunks ch
       L[r][r] += d * d;
     }
   }
-  // In-place Cholesky: A = L L^T.
+  // In-place Cholesky: A = L L^T.  A pivot that is not positive (a camera
+  // with no observation and D = NULL) raises the status word and leaves
+  // the block's inverse zero.
+  bool ok = true;
 #pragma unroll
   for (int j = 0; j < S0; ++j) {
     double djj = L[j][j];
 #pragma unroll
     for (int k = 0; k < j; ++k) djj -= L[j][k] * L[j][k];
+    ok = ok && PivotOk(djj);
     const double ljj = sqrt(djj);
     const double inv = 1.0 / ljj;
     L[j][j] = ljj;
@@ -523,8 +549,13 @@ __global__ __launch_bounds__(64) void SchurBlockInvertKernel(const GradChunks ch
       L[r][j] = v * inv;
     }
   }
-  // Columns of the inverse: L y = e_c, then L^T x = y.
   double* out = P + (int64_t)S0 * S0 * p;
+  if (!ok) {
+    *status = 1;
+    for (int k = 0; k < S0 * S0; ++k) out[k] = 0.0;
+    return;
+  }
+  // Columns of the inverse: L y = e_c, then L^T x = y.
 #pragma unroll
   for (int cc = 0; cc < S0; ++cc) {
     double y[S0];

@@ -288,7 +288,11 @@ int cse_schur_structure(cse_evaluator* ev, int64_t* num_cols_e, int64_t* num_col
  * 53-99) plus Preconditioner::Update: binds d_jacobian_values, d_D
  * (num_effective_parameters entries, may be NULL) and d_b (num_residuals)
  * -- they must stay valid until the next init -- computes the per-point
- * (E^T E + D_e^2)^-1, writes rhs (num_cols_f) and builds the preconditioner. */
+ * (E^T E + D_e^2)^-1, writes rhs (num_cols_f) and builds the preconditioner.
+ * With d_D NULL a block can be singular (a point seen by one residual block,
+ * a camera without observations): a Cholesky pivot that is not positive
+ * leaves that block's inverse zero and makes the next cse_wait return
+ * CSE_EVALUATION_FAILED, where Eigen's LLT would spread NaN silently. */
 int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
                    const double* d_b, double* d_rhs, int preconditioner);
 

@@ -83,3 +83,22 @@ def test_product_library_reads_no_environment():
     syms = subprocess.run(["nm", "-D", "--undefined-only", _cse.LIB_PATH], capture_output=True,
                           text=True, check=True).stdout
     assert "getenv" not in syms
+
+
+def test_create_rejects_unknown_gradient_mode_without_a_gpu():
+    """cse_options.gradient_mode has four meanings (0..3); anything else is
+    refused before any HIP call instead of silently running as mode 1."""
+    from ceres_amd import _cse
+    L = _cse.lib()
+    h = ctypes.c_void_p()
+    d = _cse.cse_problem_desc()
+    d.abi_version = _cse.CSE_ABI_VERSION
+    layout = (ctypes.c_int64 * 1)(0)
+    d.residual_layout = ctypes.cast(layout, _cse.P_i64)
+    for mode in (-1, 4, 7):
+        o = _cse.cse_options()
+        L.cse_default_options(ctypes.byref(o))
+        o.gradient_mode = mode
+        assert L.cse_create(ctypes.byref(d), ctypes.byref(o), ctypes.byref(h)) == _cse.CSE_ERR_INVALID
+        assert "gradient_mode" in _cse.last_error()
+        assert not h.value

@@ -116,3 +116,27 @@ def test_point_bucket_cuts_properties():
         assert all(b % 4 == 0 for b in bc[1:-1])
         for r in range(1, world):
             assert abs(bc[r] - len(pt) * r // world) <= 64 * 40
+
+
+def test_point_bucket_cuts_small_and_skewed_problems():
+    # alignment must never empty or overrun a rank.  About 100
+    # points over 8 ranks, with a few heavy points (skewed buckets).
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
+    from ceres_amd import shard
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        P = int(rng.integers(90, 120))
+        counts = rng.integers(1, 4, P)
+        counts[rng.integers(0, P, 3)] += rng.integers(10, 40, 3)
+        pt = np.repeat(np.arange(P), counts)
+        for world in (2, 3, 8):
+            pc, bc = shard.point_bucket_cuts(pt, P, world)
+            sizes = np.diff(bc)
+            assert (sizes > 0).all(), (trial, world, bc)
+            assert bc[0] == 0 and bc[-1] == len(pt) and pc[-1] == P
+            for r in range(1, world):
+                # each cut stays below the next rank's balanced target
+                assert bc[r] < len(pt) * (r + 1) // world or bc[r] == bc[r - 1] + sizes[r - 1]
+                if 0 < bc[r] < len(pt):
+                    assert pt[bc[r] - 1] < pt[bc[r]]

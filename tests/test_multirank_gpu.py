@@ -28,7 +28,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, fmt, counts, q):
+def _worker(rank, world, port, fmt, counts, q, side_stream=False):
     import sys
     for p in (os.path.join(REPO, "ceres-solver-cuda_amd"), os.path.join(REPO, "oracle"),
               os.path.join(REPO, "tests")):
@@ -45,8 +45,11 @@ def _worker(rank, world, port, fmt, counts, q):
         cams, pts, ci, pi, obs = bal.synthetic(C, P, Obs, seed=33)
         loss = ca.Loss.huber(1.0)
         torch.cuda.set_device(0)
+        # side_stream: the evaluator runs on a non-default stream, so the
+        # exchange must be ordered against that stream.
+        stream = torch.cuda.Stream() if side_stream else None
         se = distributed.ShardedEvaluator(cams, pts, ci, pi, obs, rank, world, device=0,
-                                          loss=loss, format=fmt, gradient=True)
+                                          loss=loss, format=fmt, gradient=True, stream=stream)
         for _ in range(2):  # the second evaluation re-uses every buffer
             se.evaluate()
         status = se.wait()
@@ -92,8 +95,9 @@ def _worker(rank, world, port, fmt, counts, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fmt", ["block_sparse", "compressed_row"])
-def test_sharded_libcse_matches_unsharded_oracle(gpu, fmt):
+@pytest.mark.parametrize("fmt,side_stream", [("block_sparse", False), ("compressed_row", False),
+                                             ("block_sparse", True)])
+def test_sharded_libcse_matches_unsharded_oracle(gpu, fmt, side_stream):
     import torch.multiprocessing as mp
     world = 2
     ctx = mp.get_context("spawn")
@@ -101,7 +105,7 @@ def test_sharded_libcse_matches_unsharded_oracle(gpu, fmt):
     port = _free_port()
     # Ragged shards: neither cut lands on a 64-block chunk boundary.
     counts = (20, 3001, 21113)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, counts, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, counts, q, side_stream))
              for r in range(world)]
     for p in procs:
         p.start()

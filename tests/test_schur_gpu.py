@@ -164,3 +164,27 @@ def test_schur_refuses_other_structures(gpu):
     with pytest.raises(RuntimeError, match="cse_schur_structure"):
         ev.schur_structure()
     ev.close()
+
+
+def test_schur_init_reports_singular_blocks_without_D(gpu):
+    """with d_D = NULL a point seen by one residual block has a
+    singular E^T E (rank 2).  The init must not spread NaN silently: the
+    block's inverse is zero and the next cse_wait reports the failure; with
+    a positive D the same problem factors cleanly."""
+    prog = runs_problem()  # has points with a single observation
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
+    ok, cost, r, g, jv = ev.evaluate()
+    assert ok
+    e_cols, f_cols = ev.schur_structure()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dj, db = t(jv), t(-r)
+    rhs = torch.empty(f_cols, dtype=torch.float64, device=dev)
+    ev.schur_init_device(dj.data_ptr(), None, db.data_ptr(), rhs.data_ptr(), _cse.SCHUR_JACOBI)
+    assert ev.wait() == _cse.CSE_EVALUATION_FAILED
+    assert torch.isfinite(rhs).all()
+    dD = t(np.full(prog.num_effective_parameters, 0.5))
+    ev.schur_init_device(dj.data_ptr(), dD.data_ptr(), db.data_ptr(), rhs.data_ptr(),
+                         _cse.SCHUR_JACOBI)
+    assert ev.wait() == _cse.CSE_OK
+    ev.close()
