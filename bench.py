@@ -432,6 +432,34 @@ def main():
                     "headline value)"}
         del hres, hjac
 
+        if world == 1 and args.scaling == "strong":
+            # The reference's seam served by one process over every visible
+            # device (cse_create_multi): point-bucket shards, each device's
+            # residual and Jacobian strips copied into the caller's one host
+            # buffer (page-locked on the first call), cost and gradient summed
+            # over the shards on the host.
+            devices = list(range(ndev))
+            mev = ca.Evaluator(prog, devices=devices, profile=True)
+            bufs = (np.empty(prog.num_residuals), None, np.empty(prog.num_jacobian_values))
+            hs = max(2, args.host_steps)
+            mev.evaluate(residuals=True, gradient=False, jacobian=True, out=bufs)  # registers
+            t0 = time.perf_counter()
+            for _ in range(hs):
+                ok = mev.evaluate(residuals=True, gradient=False, jacobian=True, out=bufs)[0]
+                assert ok
+            e = time.perf_counter() - t0
+            first, _ = mev.shard_info()
+            mev.close()
+            secondary["host_multi"] = {
+                "value": hs / e, "unit": "evals/s", "ms_per_step": e / hs * 1e3, "steps": hs,
+                "devices": devices, "shard_first_blocks": [int(x) for x in first],
+                "d2h_bytes": 8 * (prog.num_residuals + prog.num_jacobian_values),
+                "d2h_GBps": 8 * (prog.num_residuals + prog.num_jacobian_values) * hs / e / 1e9,
+                "what": "cse_evaluate on a cse_create_multi evaluator over every visible device "
+                        "(host state in, residuals + Jacobian values out in the caller's one host "
+                        "buffer; PCIe-inclusive, not the headline value)"}
+            del bufs
+
     out = None
     if rank == 0:
         cpu = None

@@ -143,6 +143,9 @@ SIGNATURES = {
     "cse_schur_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_schur_precondition": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_schur_back_substitute": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cse_create_multi": (C.c_int, [C.POINTER(cse_problem_desc), C.POINTER(cse_options),
+                                   P_i32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "cse_shard_info": (C.c_int, [C.c_void_p, P_i32, P_i64, P_i32]),
     "cse_destroy": (None, [C.c_void_p]),
     "cse_last_error": (C.c_char_p, []),
     "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),

@@ -348,7 +348,12 @@ class Evaluator:
     """ProgramEvaluatorCUDA seam over libcse.so (program_evaluator_cuda.h:65-183)."""
 
     def __init__(self, program, device=-1, check_finite=True, apply_loss_function=True,
-                 force_general_layout=False, profile=False, stream=None, gradient_mode=0):
+                 force_general_layout=False, profile=False, stream=None, gradient_mode=0,
+                 devices=None):
+        """devices: a list of HIP ordinals -> one evaluator over several
+        devices (cse_create_multi: point-bucket shards, strips copied into
+        the caller's one host buffer); repeats put several shards on one
+        device.  Only the host-pointer calls work on it."""
         self.program = program
         self.desc = program.descriptor()
         opts = _cse.cse_options()
@@ -366,7 +371,14 @@ class Evaluator:
         opts.use_stream = int(stream is not None)
         opts.stream = stream if stream else None
         h = C.c_void_p()
-        _cse.check(L.cse_create(C.byref(self.desc), C.byref(opts), C.byref(h)), "cse_create")
+        if devices is None:
+            _cse.check(L.cse_create(C.byref(self.desc), C.byref(opts), C.byref(h)), "cse_create")
+        else:
+            if stream is not None:
+                raise ValueError("a multi-device evaluator runs on its own per-device streams")
+            devs = (C.c_int32 * len(devices))(*devices)
+            _cse.check(L.cse_create_multi(C.byref(self.desc), C.byref(opts), devs, len(devices),
+                                          C.byref(h)), "cse_create_multi")
         self.handle = h
 
     def close(self):
@@ -385,14 +397,28 @@ class Evaluator:
         _cse.check(_cse.lib().cse_get_info(self.handle, C.byref(inf)), "cse_get_info")
         return inf
 
-    def evaluate(self, state=None, residuals=True, gradient=True, jacobian=True):
-        """Host-pointer Evaluate.  Returns (ok, cost, residuals, gradient, jacobian)."""
+    def shard_info(self):
+        """(first block of each shard + the end, device of each shard)."""
+        L = _cse.lib()
+        n = C.c_int32()
+        _cse.check(L.cse_shard_info(self.handle, C.byref(n), None, None), "cse_shard_info")
+        first = np.empty(n.value + 1, np.int64)
+        devs = np.empty(n.value, np.int32)
+        _cse.check(L.cse_shard_info(self.handle, C.byref(n), _ptr(first, C.c_int64),
+                                    _ptr(devs, C.c_int32)), "cse_shard_info")
+        return first, devs
+
+    def evaluate(self, state=None, residuals=True, gradient=True, jacobian=True, out=None):
+        """Host-pointer Evaluate.  Returns (ok, cost, residuals, gradient, jacobian).
+        out: optional (r, g, j) float64 arrays to write into (None entries are
+        allocated), e.g. buffers kept across calls."""
         p = self.program
         state = np.ascontiguousarray(p.state if state is None else state, np.float64)
         cost = C.c_double(-1.0)
-        r = np.empty(p.num_residuals) if residuals else None
-        g = np.empty(p.num_effective_parameters) if gradient else None
-        j = np.empty(p.num_jacobian_values) if jacobian else None
+        ro, go, jo = out if out is not None else (None, None, None)
+        r = (ro if ro is not None else np.empty(p.num_residuals)) if residuals else None
+        g = (go if go is not None else np.empty(p.num_effective_parameters)) if gradient else None
+        j = (jo if jo is not None else np.empty(p.num_jacobian_values)) if jacobian else None
         rc = _cse.lib().cse_evaluate(self.handle, _ptr(state, C.c_double), C.byref(cost),
                                      _ptr(r, C.c_double), _ptr(g, C.c_double), _ptr(j, C.c_double))
         _cse.check(rc, "cse_evaluate")

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/cse.h"
+#include "multi_device.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
 #include "pipeline_launch.h"
@@ -36,6 +37,15 @@ int Fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
+
+// Entry points whose arguments are device pointers of one device.
+#define CSE_SINGLE_DEVICE(ev, what)                                                         \
+  do {                                                                                     \
+    if ((ev) && (ev)->multi)                                                               \
+      return Fail(CSE_ERR_UNSUPPORTED, std::string(what) +                                 \
+                                           ": not available on a multi-device evaluator " \
+                                           "(cse_create_multi): its outputs span devices"); \
+  } while (0)
 
 #define CSE_HIP(call)                                                              \
   do {                                                                             \
@@ -419,7 +429,21 @@ LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
 
 }  // namespace
 
+int CseFail(int code, const std::string& msg) { return Fail(code, msg); }
+
+bool CseKindShape(int kind, int* num_residuals, int* num_blocks, int* data_size) {
+  KindShape k;
+  if (!ShapeOf(kind, &k)) return false;
+  *num_residuals = k.nr;
+  *num_blocks = k.nb;
+  *data_size = k.data;
+  return true;
+}
+
 struct cse_evaluator {
+  // A multi-device evaluator (cse_create_multi) is a shell around CseMulti;
+  // everything below is unused then.
+  CseMulti* multi = nullptr;
   int device = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
@@ -1250,6 +1274,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
 int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost,
                         double* d_residuals, double* d_gradient, double* d_jacobian_values) {
   if (!ev || !d_cost) return Fail(CSE_ERR_INVALID, "null evaluator or cost");
+  CSE_SINGLE_DEVICE(ev, "cse_evaluate_device");
   if (ev->num_parameters > 0 && !d_state) return Fail(CSE_ERR_INVALID, "null state");
   if (hipSetDevice(ev->device) != hipSuccess) return Fail(CSE_ERR_HIP, "hipSetDevice failed");
   return Enqueue(ev, d_state, d_cost, d_residuals, d_gradient, d_jacobian_values);
@@ -1257,6 +1282,7 @@ int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost
 
 int cse_wait(cse_evaluator* ev) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return CSE_OK;  // cse_evaluate on it is synchronous
   CSE_HIP(hipMemcpyAsync(ev->status_host, ev->status.p + 1, sizeof(int), hipMemcpyDeviceToHost,
                          ev->stream));
   CSE_HIP(hipStreamSynchronize(ev->stream));
@@ -1270,6 +1296,10 @@ int cse_wait(cse_evaluator* ev) {
 int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* residuals,
                  double* gradient, double* jacobian_values) {
   if (!ev || !cost) return Fail(CSE_ERR_INVALID, "null evaluator or cost");
+  if (ev->multi) {
+    if (!state) return Fail(CSE_ERR_INVALID, "null state");
+    return MultiEvaluate(ev->multi, state, cost, residuals, gradient, jacobian_values);
+  }
   if (ev->num_parameters > 0 && !state) return Fail(CSE_ERR_INVALID, "null state");
   CSE_HIP(hipSetDevice(ev->device));
   int rc;
@@ -1302,6 +1332,7 @@ int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* r
 
 int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return MultiSetPlusJacobians(ev->multi, plus_jacobians);
   if (ev->num_plus_jacobian_values == 0) return CSE_OK;
   if (!plus_jacobians) return Fail(CSE_ERR_INVALID, "null plus_jacobians");
   CSE_HIP(hipSetDevice(ev->device));
@@ -1340,6 +1371,7 @@ bool DispatchMultiply(int kind, const cse::GroupArgs& a, bool affine, bool left,
 
 int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double* y, bool left) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  CSE_SINGLE_DEVICE(ev, "cse_jacobian_multiply");
   if (!ev->has_layout)
     return Fail(CSE_ERR_INVALID, "the descriptor had no Jacobian layout");
   if (!J || !x || !y) return Fail(CSE_ERR_INVALID, "null pointer");
@@ -1397,6 +1429,7 @@ int cse_jacobian_left_multiply(cse_evaluator* ev, const double* d_jacobian_value
 int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
                       const double* d_x, double* d_y) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  CSE_SINGLE_DEVICE(ev, "cse_cgnr_multiply");
   if (!ev->has_layout) return Fail(CSE_ERR_INVALID, "the descriptor had no Jacobian layout");
   if (!d_jacobian_values || !d_x || !d_y) return Fail(CSE_ERR_INVALID, "null pointer");
   CSE_HIP(hipSetDevice(ev->device));
@@ -1506,6 +1539,7 @@ int SchurFTail(cse_evaluator* ev, double* y, hipStream_t s) {
 
 int SchurCheck(cse_evaluator* ev, bool need_ready) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  CSE_SINGLE_DEVICE(ev, "cse_schur");
   if (!ev->schur.eligible)
     return Fail(CSE_ERR_UNSUPPORTED,
                 "implicit Schur complement: needs one Snavely group on the affine BlockSparse path "
@@ -1632,6 +1666,7 @@ int cse_schur_back_substitute(cse_evaluator* ev, const double* d_x, double* d_y)
 int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_delta,
                     double* d_state_plus_delta) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  CSE_SINGLE_DEVICE(ev, "cse_plus_device");
   if (!ev->plus_supported)
     return Fail(CSE_ERR_UNSUPPORTED, "Plus on device: an active parameter block has a manifold");
   if (ev->plus_runs_host.empty()) return CSE_OK;
@@ -1653,6 +1688,7 @@ int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_de
 int cse_plus(cse_evaluator* ev, const double* state, const double* delta,
              double* state_plus_delta) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return MultiPlus(ev->multi, state, delta, state_plus_delta);
   if (!ev->plus_supported)
     return Fail(CSE_ERR_UNSUPPORTED, "Plus on device: an active parameter block has a manifold");
   if (ev->num_parameters == 0) return CSE_OK;
@@ -1676,6 +1712,11 @@ int cse_plus(cse_evaluator* ev, const double* state, const double* delta,
 
 void cse_destroy(cse_evaluator* ev) {
   if (!ev) return;
+  if (ev->multi) {
+    MultiDestroy(ev->multi);
+    delete ev;
+    return;
+  }
   (void)hipSetDevice(ev->device);
   if (ev->stream) (void)hipStreamSynchronize(ev->stream);
   if (ev->status_host) (void)hipHostFree(ev->status_host);
@@ -1688,8 +1729,41 @@ void cse_destroy(cse_evaluator* ev) {
   delete ev;  // every DevBuf (groups, plans, tables, scratch) frees itself
 }
 
+int cse_create_multi(const cse_problem_desc* d, const cse_options* options, const int32_t* devices,
+                     int32_t num_devices, cse_evaluator** out) {
+  if (!out) return Fail(CSE_ERR_INVALID, "null out");
+  *out = nullptr;
+  int rc = Validate(d);
+  if (rc) return rc;
+  if (options && (options->gradient_mode < 0 || options->gradient_mode > 3))
+    return Fail(CSE_ERR_INVALID, "gradient_mode " + std::to_string(options->gradient_mode) +
+                                     " is not one of 0..3");
+  cse_evaluator* ev = new (std::nothrow) cse_evaluator();
+  if (!ev) return Fail(CSE_ERR_OOM, "host allocation failed");
+  if ((rc = MultiCreate(d, options, devices, num_devices, &ev->multi))) {
+    delete ev;
+    return rc;
+  }
+  ev->device = devices[0];
+  *out = ev;
+  return CSE_OK;
+}
+
+int cse_shard_info(cse_evaluator* ev, int32_t* num_shards, int64_t* first_block, int32_t* devices) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return MultiShardInfo(ev->multi, num_shards, first_block, devices);
+  if (num_shards) *num_shards = 1;
+  if (first_block) {
+    first_block[0] = 0;
+    first_block[1] = ev->num_residual_blocks;
+  }
+  if (devices) devices[0] = ev->device;
+  return CSE_OK;
+}
+
 int cse_get_info(cse_evaluator* ev, cse_info* info) {
   if (!ev || !info) return Fail(CSE_ERR_INVALID, "null argument");
+  if (ev->multi) return MultiInfo(ev->multi, info);
   std::memset(info, 0, sizeof(*info));
   info->num_residual_blocks = ev->num_residual_blocks;
   info->num_residuals = ev->num_residuals;
@@ -1710,6 +1784,7 @@ int cse_get_info(cse_evaluator* ev, cse_info* info) {
 
 int cse_kernel_stats(cse_evaluator* ev, double* last_ms, double* total_ms, int64_t* launches) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return MultiKernelStats(ev->multi, last_ms, total_ms, launches);
   if (!ev->opts.profile) return Fail(CSE_ERR_INVALID, "evaluator created without options.profile");
   int rc = FoldTiming(ev);
   if (rc) return rc;
@@ -1721,6 +1796,7 @@ int cse_kernel_stats(cse_evaluator* ev, double* last_ms, double* total_ms, int64
 
 int cse_reset_kernel_stats(cse_evaluator* ev) {
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return MultiResetKernelStats(ev->multi);
   int rc = FoldTiming(ev);
   if (rc) return rc;
   ev->last_ms = ev->total_ms = 0.0;

@@ -307,6 +307,40 @@ int cse_schur_precondition(cse_evaluator* ev, const double* d_x, double* d_y);
  * (num_effective_parameters) = [(E^T E + D_e^2)^-1 E^T (b - F x); x]. */
 int cse_schur_back_substitute(cse_evaluator* ev, const double* d_x, double* d_y);
 
+/* ---- One host solve, several GPUs --------------------------------------
+ * The reference evaluates on one device (ContextImpl's single stream,
+ * include/ceres/internal/cuda_buffer.h:98) and Ceres' host solve calls one
+ * RegisteredCUDAEvaluators::Evaluate with host pointers
+ * (include/ceres/internal/registered_cuda_evaluators.h:75-79).
+ * cse_create_multi builds such an evaluator over several devices (SURVEY.md
+ * §8(b) "device list", §8(e)): the residual blocks are cut into num_devices
+ * contiguous shards at point-bucket boundaries (a block whose last parameter
+ * block differs from the previous block's; multiples of 4 blocks where
+ * possible), each shard is evaluated on devices[k] (repeats allowed: several
+ * shards on one device), and cse_evaluate on the returned handle
+ *   - copies each shard's residual and Jacobian-value strips straight into
+ *     disjoint regions of the caller's one residuals / jacobian_values
+ *     buffers, concurrently per device (the buffers, and the state, are
+ *     page-locked with hipHostRegister on first use and stay so until
+ *     cse_destroy or until another buffer is passed in the same role);
+ *   - sums the cost and the gradient over the shards in shard order on the
+ *     host (deterministic; a parameter block used by several shards, e.g. a
+ *     camera, gets the sum of their rows).
+ * options->use_stream and options->stream must be 0 (each device gets its
+ * own stream).  On such a handle cse_evaluate, cse_wait (returns CSE_OK),
+ * cse_plus, cse_set_plus_jacobians, cse_get_info (sizes of the whole
+ * problem; bytes summed over the shards), cse_kernel_stats (the slowest
+ * shard), cse_shard_info and cse_destroy work; the device-pointer entry
+ * points return CSE_ERR_UNSUPPORTED. */
+int cse_create_multi(const cse_problem_desc* desc, const cse_options* options,
+                     const int32_t* devices, int32_t num_devices, cse_evaluator** out);
+
+/* The shards of an evaluator: *num_shards; first_block[num_shards + 1] (may be
+ * NULL) = the residual-block ranges [first_block[k], first_block[k+1]);
+ * devices[num_shards] (may be NULL).  A cse_create evaluator has one shard. */
+int cse_shard_info(cse_evaluator* ev, int32_t* num_shards, int64_t* first_block,
+                   int32_t* devices);
+
 void cse_destroy(cse_evaluator* ev);
 
 /* Thread-local description of the last error. */

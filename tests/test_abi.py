@@ -102,3 +102,23 @@ def test_create_rejects_unknown_gradient_mode_without_a_gpu():
         assert L.cse_create(ctypes.byref(d), ctypes.byref(o), ctypes.byref(h)) == _cse.CSE_ERR_INVALID
         assert "gradient_mode" in _cse.last_error()
         assert not h.value
+
+
+def test_create_multi_rejects_bad_device_lists_without_a_gpu():
+    """cse_create_multi validates the descriptor and the device list before
+    any HIP call."""
+    from ceres_amd import _cse
+    L = _cse.lib()
+    h = ctypes.c_void_p()
+    d = _cse.cse_problem_desc()
+    d.abi_version = _cse.CSE_ABI_VERSION
+    layout = (ctypes.c_int64 * 1)(0)
+    d.residual_layout = ctypes.cast(layout, _cse.P_i64)
+    assert L.cse_create_multi(ctypes.byref(d), None, None, 2, ctypes.byref(h)) == _cse.CSE_ERR_INVALID
+    devs = (ctypes.c_int32 * 1)(0)
+    assert L.cse_create_multi(ctypes.byref(d), None, devs, 0, ctypes.byref(h)) == _cse.CSE_ERR_INVALID
+    assert "no devices" in _cse.last_error()
+    bad = _cse.cse_problem_desc()
+    bad.abi_version = 999
+    assert L.cse_create_multi(ctypes.byref(bad), None, devs, 1, ctypes.byref(h)) == _cse.CSE_ERR_INVALID
+    assert not h.value
