@@ -202,8 +202,9 @@ struct Group {
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
 
-// Cost reduction: above this many per-wave partials, a first pass of
-// kPartialBlocks workgroups shortens the serial tail of FinalizeKernel.
+// Cost reduction: above this many per-wave partials, kPartialBlocks
+// workgroups sum slices and the last of them finalises
+// (ReduceFinalizeKernel); below, one FinalizeKernel.
 constexpr int64_t kPartialsTwoPass = 4096;
 constexpr int kPartialBlocks = 128;
 
@@ -239,6 +240,13 @@ void LaunchPipelined(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   static_assert(std::is_same<K, cse::SnavelyKind>::value, "Snavely only");
   (void)num_wg;
   cse::LaunchPipelinedSnavely<L, kStoreWaves, kOpt>(a, s);
+}
+
+template <class K, int L, int kWG, int kPerCu>
+void LaunchResidualStreamed(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  static_assert(std::is_same<K, cse::SnavelyKind>::value, "Snavely only");
+  (void)num_wg;
+  cse::LaunchResidualStreamedSnavely<L, kWG, kPerCu>(a, s);
 }
 
 template <class K, int L, int kStoreWaves, int kOpt = 0>
@@ -340,6 +348,10 @@ LaunchFn TuningVariant(int v, bool jac) {
       case 26: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16>>;
       case 27: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 0, true>>;
       case 28: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, false, 0, 64, 0, false, false, 0, 16, true>>;
+      // persistent prefetching waves (pipeline.hip): 8 waves x 2 / 16 x 1 / 4 x 4 per CU
+      case 60: return &LaunchResidualStreamed<K, L, 8, 2>;
+      case 61: return &LaunchResidualStreamed<K, L, 16, 1>;
+      case 62: return &LaunchResidualStreamed<K, L, 4, 4>;
       default: return nullptr;
     }
   }
@@ -468,7 +480,7 @@ struct cse_evaluator {
   std::vector<cse::PlusRun> plus_runs_host;
   DevBuf<cse::PlusRun> plus_runs;
   DevBuf<double> h_delta, h_plus;
-  DevBuf<int> status;  // [0] running flag, [1] last status
+  DevBuf<int> status;  // [0] running flag, [1] last status, [2] reduce counter
   // Host-path buffers (allocated on first use).
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
   DevBuf<double> cg_z;  // cse_cgnr_multiply's z = J x when it cannot fuse
@@ -979,9 +991,10 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
-      const int64_t total = G.slot0_count * G.packed_stride;
+      const int pieces = (G.shape.s0 + 1) / 2;
+      const int64_t total = G.slot0_count * pieces;
       hipLaunchKernelGGL(cse::RepackSlot0Kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                         ev->stream, d_state, G.state_base[0], G.shape.s0, G.packed_stride,
+                         ev->stream, d_state, G.state_base[0], G.shape.s0, G.packed_stride, pieces,
                          G.slot0_lo, G.slot0_count, G.packed0.p);
     }
     fn(a, G.num_wg, ev->stream);
@@ -1020,17 +1033,18 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     ev->pending.push_back(timing);
   }
   const double* parts = ev->partials.p;
-  int64_t nparts = ev->total_wg;
+  const int64_t nparts = ev->total_wg;
   if (nparts > kPartialsTwoPass) {
-    // Two-pass, still fixed-order: kPartialBlocks sums, then one.
+    // Fixed-order slices summed by kPartialBlocks workgroups, the last of
+    // which adds the slice sums: one launch (ReduceFinalizeKernel).
     const int64_t per = (nparts + kPartialBlocks - 1) / kPartialBlocks;
-    hipLaunchKernelGGL(cse::PartialSumKernel, dim3(kPartialBlocks), dim3(cse::kBlockThreads), 0,
-                       ev->stream, parts, nparts, per, ev->partials2.p);
-    parts = ev->partials2.p;
-    nparts = kPartialBlocks;
+    hipLaunchKernelGGL(cse::ReduceFinalizeKernel, dim3(kPartialBlocks), dim3(cse::kBlockThreads), 0,
+                       ev->stream, parts, nparts, per, ev->partials2.p, ev->status.p + 2, d_cost,
+                       ev->status.p, ev->status.p + 1);
+  } else {
+    hipLaunchKernelGGL(cse::FinalizeKernel, dim3(1), dim3(1024), 0, ev->stream, parts, nparts,
+                       d_cost, ev->status.p, ev->status.p + 1);
   }
-  hipLaunchKernelGGL(cse::FinalizeKernel, dim3(1), dim3(1024), 0, ev->stream, parts, nparts,
-                     d_cost, ev->status.p, ev->status.p + 1);
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }
@@ -1261,8 +1275,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   if (hipMemsetAsync(ev->partials.p, 0, ev->partials.n * sizeof(double), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "hipMemsetAsync failed"));
   if ((rc = ev->partials2.alloc(kPartialBlocks))) return bail(rc);
-  if ((rc = ev->status.alloc(2))) return bail(rc);
-  if (hipMemsetAsync(ev->status.p, 0, 2 * sizeof(int), s) != hipSuccess)
+  // [0] running flag, [1] last status, [2] ReduceFinalizeKernel's counter
+  if ((rc = ev->status.alloc(3))) return bail(rc);
+  if (hipMemsetAsync(ev->status.p, 0, 3 * sizeof(int), s) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "memset failed"));
   if (hipHostMalloc(&ev->status_host, sizeof(int)) != hipSuccess)
     return bail(Fail(CSE_ERR_HIP, "hipHostMalloc failed"));

@@ -506,20 +506,6 @@ __global__ __launch_bounds__(kBlockThreads) void PlusKernel(const double* x, con
   }
 }
 
-// First pass of the cost reduction when there are many partials: workgroup
-// b sums partials [b*per, (b+1)*per) in a fixed order.
-__global__ __launch_bounds__(kBlockThreads) void PartialSumKernel(const double* partials,
-                                                                  int64_t n, int64_t per,
-                                                                  double* out) {
-  __shared__ double lds_sum[kWavesPerBlock];
-  const int64_t begin = (int64_t)blockIdx.x * per;
-  const int64_t end = begin + per < n ? begin + per : n;
-  double v = 0.0;
-  for (int64_t k = begin + threadIdx.x; k < end; k += kBlockThreads) v += partials[k];
-  const double t = WorkgroupSum(v, lds_sum);
-  if (threadIdx.x == 0) out[blockIdx.x] = t;
-}
-
 // Sums the per-workgroup partials of every group in a fixed order, writes
 // the cost, publishes the evaluation status and re-arms the status word
 // for the next evaluation (replaces thrust::reduce + the abort-flag round
@@ -554,17 +540,67 @@ __global__ __launch_bounds__(1024) void FinalizeKernel(const double* partials, i
   }
 }
 
+// Many partials, one launch: workgroup b sums partials [b*per, (b+1)*per)
+// in a fixed order and hands its sum over to
+// whichever workgroup finishes last, which adds the G slice sums in slice
+// order and finalises as FinalizeKernel does -- the same value, bit for bit,
+// as a slice pass followed by FinalizeKernel over the 128 slice sums.  Hand-over (MI355X_MICROARCH.md, valid
+// forms: one lane per storing workgroup, agent-scope atomic add, the last
+// adder told by the returned value): the slice sum is stored write-through
+// (sc1) and drained (vmcnt(0)) before the add; the last workgroup reads the
+// sums with sc1 loads only after its add has returned.  The counter is left
+// at 0 for the next launch.
+__global__ __launch_bounds__(kBlockThreads) void ReduceFinalizeKernel(
+    const double* partials, int64_t n, int64_t per, double* slices, int* counter, double* cost,
+    int* status, int* status_out) {
+  __shared__ double lds_sum[kWavesPerBlock];
+  __shared__ int last;
+  const int64_t begin = (int64_t)blockIdx.x * per;
+  const int64_t end = begin + per < n ? begin + per : n;
+  double v = 0.0;
+  for (int64_t k = begin + threadIdx.x; k < end; k += kBlockThreads) v += partials[k];
+  const double t = WorkgroupSum(v, lds_sum);
+  if (threadIdx.x == 0) {
+    double* dst = slices + blockIdx.x;
+    asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" ::"v"(dst), "v"(t)
+                 : "memory");
+    const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  double s = 0.0;
+  if (threadIdx.x < gridDim.x) {
+    const double* src = slices + threadIdx.x;
+    asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(s) : "v"(src)
+                 : "memory");
+  }
+  __syncthreads();  // lds_sum is reused
+  const double total = WorkgroupSum(s, lds_sum);
+  if (threadIdx.x == 0) {
+    const int st = *status;
+    *cost = st ? 0.0 : total;
+    *status_out = st;
+    *status = 0;
+    *counter = 0;
+  }
+}
+
 // Copies slot-0 parameter blocks [lo, lo + count) of the state into the
-// packed table at a 16-byte-aligned stride (once per evaluation: 13,682
-// cameras = 1.1 MB for BAL problem-13682).
+// packed table (once per evaluation: 13,682 cameras = 1.1 MB for BAL
+// problem-13682), one 16-byte piece per thread: the first `pieces` pieces of
+// each row of `stride` doubles (the LDS-DMA gather reads no others).
 __global__ __launch_bounds__(256) void RepackSlot0Kernel(const double* state, int64_t state_base,
-                                                         int size, int stride, int32_t lo,
+                                                         int size, int stride, int pieces, int32_t lo,
                                                          int64_t count, double* packed) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t b = t / stride;
-  const int k = (int)(t - b * stride);
+  const int64_t b = t / pieces;
+  const int k = 2 * (int)(t - b * pieces);
   if (b >= count) return;
-  packed[t] = k < size ? state[state_base + (int64_t)size * (lo + b) + k] : 0.0;
+  const double* src = state + state_base + (int64_t)size * (lo + b);
+  const double x = src[k];
+  const double y = k + 1 < size ? src[k + 1] : 0.0;
+  *reinterpret_cast<double2*>(packed + (int64_t)stride * b + k) = make_double2(x, y);
 }
 
 }  // namespace cse

@@ -82,4 +82,27 @@ CSE_PIPE_INST(kLossHuber, 2)
 #undef CSE_PIPE_INST
 #undef CSE_PIPE_INST2
 
+// Residual-only / cost-only streamed kernel: kWG waves per workgroup,
+// kPerCu workgroups per CU (the LDS input buffers: 8 KiB a wave).
+template <int kLoss, int kWG, int kPerCu>
+void LaunchResidualStreamedSnavely(const GroupArgs& a, hipStream_t s) {
+  const int64_t chunks = (a.n + kWave - 1) / kWave;
+  const int64_t grid =
+      std::max<int64_t>(1, std::min<int64_t>((int64_t)a.num_cus * kPerCu, (chunks + kWG - 1) / kWG));
+  if (a.residuals)
+    hipLaunchKernelGGL((EvaluateResidualStreamed<SnavelyKind, kLoss, true, kWG>), dim3((unsigned)grid),
+                       dim3(kWG * kWave), 0, s, a);
+  else
+    hipLaunchKernelGGL((EvaluateResidualStreamed<SnavelyKind, kLoss, false, kWG>), dim3((unsigned)grid),
+                       dim3(kWG * kWave), 0, s, a);
+}
+#define CSE_RES_INST(L, G, C) template void LaunchResidualStreamedSnavely<L, G, C>(const GroupArgs&, hipStream_t);
+CSE_RES_INST(kLossHuber, 8, 2)
+CSE_RES_INST(kLossTrivial, 8, 2)
+CSE_RES_INST(kLossHuber, 16, 1)
+CSE_RES_INST(kLossTrivial, 16, 1)
+CSE_RES_INST(kLossHuber, 4, 4)
+CSE_RES_INST(kLossTrivial, 4, 4)
+#undef CSE_RES_INST
+
 }  // namespace cse

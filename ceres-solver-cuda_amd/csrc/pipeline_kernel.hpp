@@ -397,6 +397,104 @@ __global__ __launch_bounds__(kPipeThreads) void EvaluateAffinePipelined(const Gr
     PipeStoreWave<K, kStoreWaves, kOpt>(a, L, wave - P::kCompute, lane, c0, cstep, nloc);
 }
 
+// ---------------------------------------------------------------------------
+// Residual-only / cost-only evaluation (the trust-region candidate step,
+// trust_region_minimizer.cc:770-788) as persistent prefetching waves.  The
+// one-chunk-per-wave kernel spends most of a wave's life in two dependent
+// load round trips (the ids, then the camera gather); here
+// each wave walks its chunks c, c + W, c + 2W, ... (W waves in the grid)
+// with every input moved by LDS-DMA: the ids two chunks ahead, the camera
+// pieces, observation and point one chunk ahead, so a wave waits on no
+// dependent chain.  Per chunk a wave writes its residuals (kResiduals) and
+// its cost partial; the top-of-iteration wait leaves those kStores youngest
+// operations in flight (s_waitcnt vmcnt(kStores)).
+template <class K, int kLoss, bool kResiduals, int kWG>
+__global__ __launch_bounds__(kWG * kWave) void EvaluateResidualStreamed(const GroupArgs a) {
+  using P = PipeShape<K, 4>;  // the input-buffer layout only
+  using Tr = KindTraits<K>;
+  constexpr int NR = P::NR;
+  static_assert(NR == 2, "one 16-byte residual store per lane");
+  __shared__ alignas(16) double in_all[kWG][P::kInDoubles];
+  const int lane0 = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  double* in = in_all[w];
+  const int64_t num_chunks = (a.n + kWave - 1) / kWave;
+  const int64_t W = (int64_t)gridDim.x * kWG;
+  int64_t c = (int64_t)blockIdx.x * kWG + w;
+  if (c >= num_chunks) return;
+  auto block_of = [&](int64_t cc, int lane) -> int64_t {
+    const int64_t i0 = cc * kWave;
+    const int64_t rem = a.n - 1 - i0;
+    return i0 + (lane < rem ? lane : rem);
+  };
+  {
+    const int64_t i = block_of(c, lane0);
+    PipeIssueIds<K, 4>(a, in, i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    int cam, pt;
+    PipeReadIds<K, 4>(in, lane0, &cam, &pt);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    PipeIssueInputs<K, 4, 32 + 8 * kWG + kLoss + 4 * kResiduals>(a, in, i, cam - a.packed0_lo, pt, lane0);
+    if (c + W < num_chunks) PipeIssueIds<K, 4>(a, in, block_of(c + W, lane0));
+  }
+  constexpr int kStores = kResiduals ? 2 : 1;  // residual pair + lane-0 partial
+  bool first = true;
+  for (; c < num_chunks; c += W) {
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    if (first)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStores) : "memory");
+    first = false;
+    __builtin_amdgcn_wave_barrier();
+    AffineInputs<K> x;
+    {
+      const double* cam = in + P::kInCam + lane * P::S0p;
+#pragma unroll
+      for (int k = 0; k < P::S0; ++k) x.x0[k] = cam[k];
+      const double2 o = reinterpret_cast<const double2*>(in + P::kInObs)[lane];
+      x.d[0] = o.x;
+      x.d[1] = o.y;
+      const uint32_t* h = reinterpret_cast<const uint32_t*>(in + P::kInPt) + lane;
+      x.x1[0] = __hiloint2double((int)h[kWave], (int)h[0]);
+      x.x1[1] = __hiloint2double((int)h[3 * kWave], (int)h[2 * kWave]);
+      x.x1[2] = __hiloint2double((int)h[5 * kWave], (int)h[4 * kWave]);
+    }
+    const int64_t cn = c + W;
+    int cam_n = 0, pt_n = 0;
+    if (cn < num_chunks) PipeReadIds<K, 4>(in, lane, &cam_n, &pt_n);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (cn < num_chunks) {
+      PipeIssueInputs<K, 4, 32 + 8 * kWG + kLoss + 4 * kResiduals>(a, in, block_of(cn, lane),
+                                                         cam_n - a.packed0_lo, pt_n, lane);
+      if (cn + W < num_chunks) PipeIssueIds<K, 4>(a, in, block_of(cn + W, lane));
+    }
+    const int64_t i0 = c * kWave;
+    const int64_t rem = a.n - i0;
+    const bool active = lane < rem;
+    double r[NR], J0[1], J1[1];
+    bool ok = EvaluateFunctor<K, false>(x.d, x.x0, x.x1, r, J0, J1);
+    if (ok && a.check_finite) ok = !AnyNonFinite<NR>(r);
+    const double cost = LossAndCorrect<K, kLoss, false>(a.loss, a.apply_loss, r, J0, J1, kResiduals);
+    const double wsum = WaveSumLane0(active ? cost : 0.0);
+    const bool failed = __ballot(active && !ok) != 0;
+    double* v_partial = a.partials + c;
+    double v_wsum = wsum;
+    asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
+    if constexpr (kResiduals) {
+      double* rdst = a.residuals + a.res_base + (int64_t)NR * (i0 + lane);
+      const cse_v4i q = AsV4i(r[0], r[1]);
+      if (active) StoreNt16<0>(rdst, q);
+    }
+    if (lane == 0) StoreB64(v_partial, v_wsum);
+    if (failed && lane == 0) StoreB32(a.status, 1);  // younger still: only over-waits
+  }
+}
+
 }  // namespace cse
 
 #endif  // CSE_PIPELINE_KERNEL_HPP_

@@ -17,6 +17,8 @@ namespace cse {
 // workgroup per CU (a.num_cus), at most one per chunk.
 template <int kLoss, int kStoreWaves, int kOpt = 0>
 void LaunchPipelinedSnavely(const GroupArgs& a, hipStream_t s);
+template <int kLoss, int kWG, int kPerCu>
+void LaunchResidualStreamedSnavely(const GroupArgs& a, hipStream_t s);
 #ifdef CSE_TUNING
 template <int kLoss, int kStoreWaves, int kOpt = 0>
 void LaunchPipelinedSnavelyProbe(const GroupArgs& a, hipStream_t s);
