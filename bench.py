@@ -82,6 +82,11 @@ def parse():
                          "(trust_region_minimizer.cc:770-788); spmv: one CGNR iteration's "
                          "products J p and J^T (J p); cgnr: the one-pass normal operator; "
                          "schur: one product with the implicit Schur complement (cse_schur_multiply)")
+    ap.add_argument("--camera", default="angle_axis", choices=["angle_axis", "quaternion"],
+                    help="angle_axis: SnavelyReprojectionError<2,9,3> (the headline); quaternion: "
+                         "SnavelyReprojectionErrorWithQuaternions<2,10,3> with every camera on "
+                         "ProductManifold<QuaternionManifold, EuclideanManifold<6>> "
+                         "(bundle_adjuster --use_quaternions --use_manifolds)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the gradient / residual-only / host-strip legs")
     ap.add_argument("--secondary-steps", type=int, default=20)
@@ -261,6 +266,9 @@ def main():
     t_build = time.perf_counter()
     counts = bal.CONFIGS[args.config]
     arrays = bal.synthetic(*counts, seed=args.seed + (0 if strong else rank))
+    quat = args.camera == "quaternion"
+    if quat:
+        arrays = (bal.to_quaternion_cameras(arrays[0]),) + tuple(arrays[1:])
     srank, sworld = (rank, world) if strong else (0, 1)
     if args.shard_of > 1:
         if world != 1:
@@ -270,8 +278,9 @@ def main():
     se = distributed.ShardedEvaluator(*arrays, srank, sworld, device=dev_index,
                                       loss=make_loss(args.loss), format=args.format,
                                       gradient=True, gradient_mode=args.gradient_mode,
-                                      stream=stream)
-    if not (rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "jacobian"):
+                                      stream=stream, quaternion_manifold=quat)
+    if not (rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "jacobian"
+            and not quat):
         del arrays
         arrays = None
     build_s = time.perf_counter() - t_build
@@ -470,14 +479,16 @@ def main():
             cpu = cpu_baseline(args, arrays, threads)
         traffic = None
         pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}_{args.loss}_{args.format}.json")
-        if world == 1 and args.mode == "jacobian" and not args.gradient and os.path.exists(pmc_path):
+        if (world == 1 and args.mode == "jacobian" and not args.gradient and not quat
+                and os.path.exists(pmc_path)):
             with open(pmc_path) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         C_, P_, O_ = counts
         sh = se.shard
         out = {
-            "metric": METRIC if args.mode == "jacobian" else
-                      f"{args.mode} evaluations/sec on BAL {args.config} (not the headline)",
+            "metric": METRIC if args.mode == "jacobian" and not quat else
+                      f"{args.mode} evaluations/sec on BAL {args.config}"
+                      f"{' with quaternion cameras on their manifold' if quat else ''} (not the headline)",
             "value": value,
             "unit": "evals/s",
             "n_gpus": world,
@@ -490,8 +501,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic (BAL-shaped: exact header counts, seeded generator)",
             "config": {
-                "workload": f"{args.config} SnavelyReprojectionError<2,9,3> "
-                            f"{args.loss} {args.format} "
+                "workload": f"{args.config} "
+                            + ("SnavelyReprojectionErrorWithQuaternions<2,10,3>, cameras on "
+                               "ProductManifold<QuaternionManifold, EuclideanManifold<6>> "
+                               if quat else "SnavelyReprojectionError<2,9,3> ")
+                            + f"{args.loss} {args.format} "
                             + {"jacobian": "residual+Jacobian", "residual": "residual+cost",
                                "candidate": "Plus + cost-only",
                                "spmv": "J p + J^T (J p)",
@@ -524,7 +538,7 @@ def main():
                 "kernel_ms_avg_max_rank": kernel_ms_max,
                 "kernel": f"cse::EvaluateAffineChunks"
                           f"{'FusedPoints' if args.gradient else ('TwoRound' if args.format == 'block_sparse' else '')}"
-                          f"<SnavelyKind, {args.loss}, {args.format}> (+ repack"
+                          f"<{'SnavelyQuaternionTangentKind' if quat else 'SnavelyKind'}, {args.loss}, {args.format}> (+ repack"
                           f"{', CameraGradientKernel and the gradient tail' if args.gradient else ''})",
                 "per": "GPU (bytes of all ranks / N over the slowest rank's kernel time)",
                 "traffic_source": "profiles/pmc_<config>_<loss>_<format>.json (rocprofv3 "

@@ -61,6 +61,10 @@ LOSS_TRIVIAL = 0
 LOSS_HUBER = 1
 LOSS_CAUCHY = 2
 
+# cse_manifold_kind (include/cse.h)
+MANIFOLD_MATRIX = 0
+MANIFOLD_QUATERNION_EUCLIDEAN = 1
+
 
 class cse_loss(C.Structure):
     _fields_ = [("kind", C.c_int32), ("scaled", C.c_int32), ("a", C.c_double),
@@ -69,7 +73,7 @@ class cse_loss(C.Structure):
 
 class cse_parameter_block(C.Structure):
     _fields_ = [("size", C.c_int32), ("tangent_size", C.c_int32),
-                ("is_constant", C.c_int32), ("reserved", C.c_int32),
+                ("is_constant", C.c_int32), ("manifold", C.c_int32),
                 ("state_offset", C.c_int64), ("delta_offset", C.c_int64),
                 ("plus_jacobian_offset", C.c_int64)]
 

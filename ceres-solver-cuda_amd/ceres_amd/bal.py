@@ -271,11 +271,35 @@ def schur_residual_order(pt_idx, num_points):
     return perm
 
 
-def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=_cse.SNAVELY_2_9_3,
-            format=BLOCK_SPARSE, compile=True):
+def to_quaternion_cameras(cameras):
+    """The 10-parameter cameras {q[4], t[3], f, k1, k2} of BALProblem with
+    use_quaternions (examples/bal_problem.cc:110-121): each angle-axis
+    rotation through AngleAxisToQuaternion (include/ceres/rotation.h:
+    320-352), the rest copied."""
+    cameras = np.asarray(cameras, np.float64)
+    aa = cameras[:, :3]
+    theta = np.sqrt((aa * aa).sum(axis=1))
+    nz = theta != 0.0
+    half = theta * 0.5
+    k = np.where(nz, np.sin(half) / np.where(nz, theta, 1.0), 0.5)
+    out = np.empty((cameras.shape[0], 10))
+    out[:, 0] = np.where(nz, np.cos(half), 1.0)
+    out[:, 1:4] = aa * k[:, None]
+    out[:, 4:] = cameras[:, 3:9]
+    return out
+
+
+def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=None,
+            format=BLOCK_SPARSE, compile=True, quaternion_manifold=False):
     """The Schur-ordered Program of a BAL problem (observations must
     already be point-major, as synthetic() returns and
-    schur_residual_order() produces)."""
+    schur_residual_order() produces).  10-parameter (quaternion) cameras
+    take SNAVELY_QUATERNION_2_10_3; quaternion_manifold puts each on
+    ProductManifold<QuaternionManifold, EuclideanManifold<6>>, as
+    bundle_adjuster --use_quaternions --use_manifolds does
+    (examples/bundle_adjuster.cc:337-345)."""
+    if kind is None:
+        kind = _cse.SNAVELY_QUATERNION_2_10_3 if cameras.shape[1] == 10 else _cse.SNAVELY_2_9_3
     C, P = cameras.shape[0], points.shape[0]
     cam_size = cameras.shape[1]
     npb = P + C
@@ -290,13 +314,23 @@ def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=_cse.SNAVELY_
     state = np.concatenate([points.ravel(), cameras.ravel()])
     prog = Program(pb_size, pb_size.copy(), np.zeros(npb, np.int32), np.full(npb, -1, np.int64),
                    np.zeros(0), [group], len(cam_idx), state, np.zeros(0))
+    if quaternion_manifold:
+        assert cam_size == 10, "quaternion cameras"
+        prog.pb_manifold = np.zeros(npb, np.int32)
+        prog.pb_manifold[P:] = _cse.MANIFOLD_QUATERNION_EUCLIDEAN
+        prog.pb_tangent[P:] = 9
     if compile:
         prog.compile(format, num_eliminate_blocks=P)
     return prog
 
 
 def synthetic_program(name_or_counts, loss=None, format=BLOCK_SPARSE, seed=0xCE2E5,
-                      compile=True):
+                      compile=True, quaternion=False, quaternion_manifold=False):
+    """A synthetic BAL Program; quaternion: 10-parameter cameras
+    (to_quaternion_cameras), optionally on the quaternion manifold."""
     counts = CONFIGS[name_or_counts] if isinstance(name_or_counts, str) else name_or_counts
     cams, pts, ci, pi, obs = synthetic(*counts, seed=seed)
-    return program(cams, pts, ci, pi, obs, loss=loss, format=format, compile=compile)
+    if quaternion or quaternion_manifold:
+        cams = to_quaternion_cameras(cams)
+    return program(cams, pts, ci, pi, obs, loss=loss, format=format, compile=compile,
+                   quaternion_manifold=quaternion_manifold)

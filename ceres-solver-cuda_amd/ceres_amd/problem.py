@@ -99,6 +99,8 @@ class Program:
     num_jacobian_values: int = 0
     crs_rows: np.ndarray = None
     crs_cols: np.ndarray = None
+    # cse_manifold_kind per parameter block (None = all MANIFOLD_MATRIX).
+    pb_manifold: np.ndarray = None
     _keep: list = field(default_factory=list)
 
     @property
@@ -149,7 +151,7 @@ class Program:
         npb = self.num_parameter_blocks
         arr = (_cse.cse_parameter_block * max(npb, 1))()
         rec = np.frombuffer(arr, dtype=np.dtype([("size", "<i4"), ("tangent_size", "<i4"),
-                                                  ("is_constant", "<i4"), ("reserved", "<i4"),
+                                                  ("is_constant", "<i4"), ("manifold", "<i4"),
                                                   ("state_offset", "<i8"),
                                                   ("delta_offset", "<i8"),
                                                   ("plus_jacobian_offset", "<i8")]),
@@ -158,11 +160,46 @@ class Program:
             rec["size"] = self.pb_size
             rec["tangent_size"] = self.pb_tangent
             rec["is_constant"] = self.pb_constant
-            rec["reserved"] = 0
+            rec["manifold"] = 0 if self.pb_manifold is None else self.pb_manifold
             rec["state_offset"] = self.state_offset
             rec["delta_offset"] = self.delta_offset
             rec["plus_jacobian_offset"] = self.pb_plus_jacobian
         return arr
+
+    def with_explicit_manifolds(self, state=None):
+        """The same Program with every MANIFOLD_QUATERNION_EUCLIDEAN block
+        given by its explicit plus-Jacobian matrix at `state` (default
+        self.state): what the reference uploads for such a block
+        (RegisteredCUDAEvaluators::UpdatePlusJacobians,
+        registered_cuda_evaluators.cc:139-160, from
+        ProductManifold<QuaternionManifold, EuclideanManifold<n>>::PlusJacobian).
+        Checkers on the host take this form; the library builds the matrix itself."""
+        import copy
+        if self.pb_manifold is None or not np.any(self.pb_manifold):
+            return self
+        state = self.state if state is None else np.asarray(state, np.float64)
+        out = copy.copy(self)
+        pj_off = self.pb_plus_jacobian.copy()
+        vals = [np.asarray(self.plus_jacobians, np.float64).ravel()]
+        count = vals[0].size
+        const = self.pb_constant != 0
+        for b in np.flatnonzero(self.pb_manifold == _cse.MANIFOLD_QUATERNION_EUCLIDEAN):
+            size = int(self.pb_size[b])
+            src = self.constant_state if const[b] else state
+            if self.state_offset is not None:
+                off = int(self.state_offset[b])
+            else:  # program order of the active / constant blocks
+                sel = (const == const[b]) & (np.arange(len(const)) < b)
+                off = int(self.pb_size[sel].sum())
+            P = quaternion_euclidean_plus_jacobian(src[off:off + size])
+            pj_off[b] = count
+            vals.append(P.ravel())
+            count += P.size
+        out.pb_plus_jacobian = pj_off
+        out.plus_jacobians = np.concatenate(vals)
+        out.pb_manifold = None
+        out._keep = []
+        return out
 
     def compile(self, format=BLOCK_SPARSE, num_eliminate_blocks=0):
         """Offsets (program.cc:151-177) and the Jacobian layout tables."""
@@ -256,11 +293,26 @@ class Program:
         return d
 
 
+def quaternion_euclidean_plus_jacobian(x):
+    """PlusJacobian of ProductManifold<QuaternionManifold, EuclideanManifold<n>>
+    at x (size 4 + n, tangent 3 + n): QuaternionPlusJacobianImpl
+    (internal/ceres/manifold.cc:62-78, Ceres order w, x, y, z) and an
+    identity, block-diagonal."""
+    x = np.asarray(x, np.float64)
+    size = x.size
+    P = np.zeros((size, size - 1))
+    w, qx, qy, qz = x[:4]
+    P[:4, :3] = [[-qx, -qy, -qz], [w, qz, -qy], [-qz, w, qx], [qy, -qx, w]]
+    P[4:, 3:] = np.eye(size - 4)
+    return P
+
+
 class ProblemCUDA:
     """Incremental builder with the reference's ProblemCUDA vocabulary."""
 
     def __init__(self):
         self._sizes, self._tangent, self._const, self._pj_off = [], [], [], []
+        self._manifold = []
         self._values = []
         self._pj = []
         self._pj_count = 0
@@ -273,6 +325,7 @@ class ProblemCUDA:
         self._tangent.append(values.size)
         self._const.append(0)
         self._pj_off.append(-1)
+        self._manifold.append(0)
         self._values.append(values.copy())
         return len(self._sizes) - 1
 
@@ -287,6 +340,14 @@ class ProblemCUDA:
         self._pj_off[b] = self._pj_count
         self._pj.append(pj.ravel())
         self._pj_count += pj.size
+
+    def set_quaternion_euclidean_manifold(self, b):
+        """SetManifold(b, ProductManifold<QuaternionManifold,
+        EuclideanManifold<size - 4>>): the library builds the plus-Jacobian
+        from the block's value (MANIFOLD_QUATERNION_EUCLIDEAN)."""
+        assert self._sizes[b] >= 4 and self._pj_off[b] < 0
+        self._tangent[b] = self._sizes[b] - 1
+        self._manifold[b] = _cse.MANIFOLD_QUATERNION_EUCLIDEAN
 
     def add_residual_blocks(self, kind, loss, ids, data):
         ids = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1, len(FUNCTOR_SHAPES[kind][1])))
@@ -340,8 +401,11 @@ class ProblemCUDA:
         state = np.concatenate([v for v, c in zip(values, const) if not c] or [np.zeros(0)])
         cstate = np.concatenate([v for v, c in zip(values, const) if c] or [np.zeros(0)])
         pj = np.concatenate(self._pj) if self._pj else np.zeros(0)
-        return Program(np.array(self._sizes, np.int32), np.array(self._tangent, np.int32), const,
+        prog = Program(np.array(self._sizes, np.int32), np.array(self._tangent, np.int32), const,
                        np.array(self._pj_off, np.int64), pj, groups, nrb, state, cstate)
+        if any(self._manifold):
+            prog.pb_manifold = np.array(self._manifold, np.int32)
+        return prog
 
 
 class Evaluator:

@@ -99,14 +99,14 @@ def gradient_maps(shard, num_points, num_cameras, cam_size=9, pt_size=3):
 
 
 def shard_program(cameras, points, cam_idx, pt_idx, obs, rank, world, loss=None,
-                  format=BLOCK_SPARSE, compile=True):
+                  format=BLOCK_SPARSE, compile=True, quaternion_manifold=False):
     """The rank's Program: its points (renumbered from 0), every camera, its
-    observations; same functor and loss as the full problem."""
+    observations; same functor, loss and camera manifold as the full problem."""
     pc, bc = point_bucket_cuts(pt_idx, points.shape[0], world)
     p0, p1, b0, b1 = pc[rank], pc[rank + 1], bc[rank], bc[rank + 1]
     prog = bal.program(cameras, points[p0:p1], cam_idx[b0:b1],
                        np.asarray(pt_idx[b0:b1]) - p0, obs[b0:b1], loss=loss, format=format,
-                       compile=compile)
+                       compile=compile, quaternion_manifold=quaternion_manifold)
     return prog, Shard(rank, world, (p0, p1), (b0, b1), len(cam_idx), format)
 
 

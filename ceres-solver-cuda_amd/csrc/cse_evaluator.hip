@@ -62,9 +62,15 @@ using TestLinear2_23 = cse::LinearTestKind<2, 2, 3>;
 using TestLinear3_24 = cse::LinearTestKind<3, 2, 4>;
 using TestLinear4_34 = cse::LinearTestKind<4, 3, 4>;
 
+// Internal kernel kinds (never in a descriptor): a group whose slot-0
+// blocks carry a manifold the affine kernels build in registers.
+constexpr int kKindQuaternionTangent = -100;  // SNAVELY_QUATERNION_2_10_3, slot 0 on
+                                              // CSE_MANIFOLD_QUATERNION_EUCLIDEAN
+
 template <class F>
 bool VisitKind(int kind, F&& f) {
   switch (kind) {
+    case kKindQuaternionTangent: f(cse::SnavelyQuaternionTangentKind{}); return true;
     case CSE_FUNCTOR_SNAVELY_2_9_3: f(cse::SnavelyKind{}); return true;
     case CSE_FUNCTOR_SNAVELY_NO_DISTORTION_2_7_3: f(cse::SnavelyNoDistortionKind{}); return true;
     case CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3: f(cse::SnavelyQuaternionKind{}); return true;
@@ -88,6 +94,7 @@ struct KindShape {
   int nr = 0, nb = 0, data = 0;
   int sz[cse::kMaxSlots] = {};
   int s0 = 0, s1 = 0;  // sz[0], sz[1] (0 if absent): the two-slot affine path
+  int x0 = 0;          // slot-0 values gathered (ambient; s0 is the Jacobian's columns)
 };
 
 bool ShapeOf(int kind, KindShape* k) {
@@ -100,6 +107,7 @@ bool ShapeOf(int kind, KindShape* k) {
     for (int j = 0; j < Tr::NB; ++j) k->sz[j] = K::kSizes[j];
     k->s0 = k->sz[0];
     k->s1 = Tr::NB > 1 ? k->sz[1] : 0;
+    k->x0 = Tr::X0;
   });
 }
 
@@ -267,32 +275,45 @@ void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 // The affine kernel with the fused gradient (Snavely groups): with the
 // slot-0 contributions (gradient_mode 3) or points only (gradient_mode 0,
 // slot 0 from CameraGradientKernel).
-template <int L, bool Crs>
+template <class K, int L, bool Crs>
 void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<cse::SnavelyKind, L, Crs>),
-                     dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<K, L, Crs>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
 }
-template <int L, bool Crs>
+template <class K, int L, bool Crs>
 void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<cse::SnavelyKind, L, Crs>),
-                     dim3((unsigned)num_wg), dim3(cse::kBlockThreads), 0, s, a);
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
 }
 
-LaunchFn PickFused(int loss, int policy) {
-  const bool crs = policy == kAffineCrs;
+// Kinds with the fused gradient: the Snavely camera and the quaternion
+// camera on its manifold (the same 2 x (9 + 3) Jacobian shape).
+bool FusedKind(int kind) {
+  return kind == CSE_FUNCTOR_SNAVELY_2_9_3 || kind == kKindQuaternionTangent;
+}
+
+template <class K>
+LaunchFn PickFusedK(int loss, bool crs, bool points) {
   switch (loss) {
-    case CSE_LOSS_HUBER: return crs ? &LaunchFused<cse::kLossHuber, true> : &LaunchFused<cse::kLossHuber, false>;
-    case CSE_LOSS_CAUCHY: return crs ? &LaunchFused<cse::kLossCauchy, true> : &LaunchFused<cse::kLossCauchy, false>;
-    default: return crs ? &LaunchFused<cse::kLossTrivial, true> : &LaunchFused<cse::kLossTrivial, false>;
+    case CSE_LOSS_HUBER:
+      return points ? (crs ? &LaunchFusedPoints<K, cse::kLossHuber, true> : &LaunchFusedPoints<K, cse::kLossHuber, false>)
+                    : (crs ? &LaunchFused<K, cse::kLossHuber, true> : &LaunchFused<K, cse::kLossHuber, false>);
+    case CSE_LOSS_CAUCHY:
+      return points ? (crs ? &LaunchFusedPoints<K, cse::kLossCauchy, true> : &LaunchFusedPoints<K, cse::kLossCauchy, false>)
+                    : (crs ? &LaunchFused<K, cse::kLossCauchy, true> : &LaunchFused<K, cse::kLossCauchy, false>);
+    default:
+      return points ? (crs ? &LaunchFusedPoints<K, cse::kLossTrivial, true> : &LaunchFusedPoints<K, cse::kLossTrivial, false>)
+                    : (crs ? &LaunchFused<K, cse::kLossTrivial, true> : &LaunchFused<K, cse::kLossTrivial, false>);
   }
 }
-LaunchFn PickFusedPoints(int loss, int policy) {
+
+// points = true: the slot-1 rows only (gradient_mode 0, slot 0 from
+// CameraGradientKernel); false: with the slot-0 contributions (mode 3).
+LaunchFn PickFused(int kind, int loss, int policy, bool points) {
   const bool crs = policy == kAffineCrs;
-  switch (loss) {
-    case CSE_LOSS_HUBER: return crs ? &LaunchFusedPoints<cse::kLossHuber, true> : &LaunchFusedPoints<cse::kLossHuber, false>;
-    case CSE_LOSS_CAUCHY: return crs ? &LaunchFusedPoints<cse::kLossCauchy, true> : &LaunchFusedPoints<cse::kLossCauchy, false>;
-    default: return crs ? &LaunchFusedPoints<cse::kLossTrivial, true> : &LaunchFusedPoints<cse::kLossTrivial, false>;
-  }
+  if (kind == kKindQuaternionTangent)
+    return PickFusedK<cse::SnavelyQuaternionTangentKind>(loss, crs, points);
+  return PickFusedK<cse::SnavelyKind>(loss, crs, points);
 }
 
 // Affine kernels: cooperative slot-0 gather by LDS-DMA from the repacked
@@ -425,7 +446,16 @@ LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
   LaunchFn fn = nullptr;
   VisitKind(kind, [&](auto kd) {
     using K = decltype(kd);
-    if constexpr (cse::TestOnly<K>::value) {
+    if constexpr (cse::AffineOnly<K>::value) {
+      if (policy == kAffinePacked || policy == kAffineCrs) {
+        const bool crs = policy == kAffineCrs;
+        switch (loss) {
+          case CSE_LOSS_HUBER: fn = crs ? PickAffine<K, cse::kLossHuber, true>(jac, dma) : PickAffine<K, cse::kLossHuber, false>(jac, dma); break;
+          case CSE_LOSS_CAUCHY: fn = crs ? PickAffine<K, cse::kLossCauchy, true>(jac, dma) : PickAffine<K, cse::kLossCauchy, false>(jac, dma); break;
+          default: fn = crs ? PickAffine<K, cse::kLossTrivial, true>(jac, dma) : PickAffine<K, cse::kLossTrivial, false>(jac, dma); break;
+        }
+      }
+    } else if constexpr (cse::TestOnly<K>::value) {
       if (loss == CSE_LOSS_TRIVIAL)
         fn = jac ? &LaunchTable<K, cse::kLossTrivial, true> : &LaunchTable<K, cse::kLossTrivial, false>;
     } else {
@@ -532,6 +562,14 @@ int Validate(const cse_problem_desc* d) {
         pb.plus_jacobian_offset + (int64_t)pb.size * pb.tangent_size > d->num_plus_jacobian_values)
       return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) +
                                        " plus jacobian out of range");
+    if (pb.manifold != CSE_MANIFOLD_MATRIX && pb.manifold != CSE_MANIFOLD_QUATERNION_EUCLIDEAN)
+      return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) + ": unknown manifold " +
+                                       std::to_string(pb.manifold));
+    if (pb.manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN &&
+        (pb.size < 4 || pb.tangent_size != pb.size - 1 || pb.plus_jacobian_offset >= 0))
+      return Fail(CSE_ERR_INVALID, "parameter block " + std::to_string(b) +
+                                       ": the quaternion manifold needs size >= 4, tangent_size "
+                                       "size - 1 and plus_jacobian_offset -1");
   }
   if (d->num_constant_parameters > 0 && !d->constant_state)
     return Fail(CSE_ERR_INVALID, "constant_state missing");
@@ -649,22 +687,34 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
   auto gidx = [&](int64_t i) {
     return g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
   };
-  const int sizes[2] = {k.s0, k.s1};
-  // Parameters: active, no manifold, state/delta offsets affine in the id.
+  // Ambient sizes (state offsets) and tangent sizes (delta offsets, the
+  // Jacobian's columns).  Slot 0 of the quaternion camera may be on
+  // CSE_MANIFOLD_QUATERNION_EUCLIDEAN (then in every block): the kernel kind
+  // becomes kKindQuaternionTangent, which builds the plus-Jacobian itself.
+  const int ambient[2] = {k.s0, k.s1};
+  int sizes[2] = {k.s0, k.s1};
+  int manifold[2] = {CSE_MANIFOLD_MATRIX, CSE_MANIFOLD_MATRIX};
+  if (g.functor_kind == CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 &&
+      d->parameter_blocks[g.parameter_block_ids[0]].manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
+    manifold[0] = CSE_MANIFOLD_QUATERNION_EUCLIDEAN;
+    sizes[0] = k.s0 - 1;
+  }
+  // Parameters: active, no explicit plus-Jacobian, state/delta offsets
+  // affine in the id.
   for (int j = 0; j < k.nb; ++j) {
     const int32_t id0 = g.parameter_block_ids[j];
     const cse_parameter_block& pb0 = d->parameter_blocks[id0];
-    G->state_base[j] = pb0.state_offset - (int64_t)sizes[j] * id0;
+    G->state_base[j] = pb0.state_offset - (int64_t)ambient[j] * id0;
     G->delta_base[j] = pb0.delta_offset - (int64_t)sizes[j] * id0;
   }
   for (int64_t i = 0; i < n; ++i)
     for (int j = 0; j < k.nb; ++j) {
       const int32_t id = g.parameter_block_ids[i * k.nb + j];
       const cse_parameter_block& pb = d->parameter_blocks[id];
-      if (pb.is_constant || pb.plus_jacobian_offset >= 0 || pb.tangent_size != sizes[j] ||
-          pb.size != sizes[j])
+      if (pb.is_constant || pb.plus_jacobian_offset >= 0 || pb.manifold != manifold[j] ||
+          pb.tangent_size != sizes[j] || pb.size != ambient[j])
         return kTable;
-      if (pb.state_offset != G->state_base[j] + (int64_t)sizes[j] * id) return kTable;
+      if (pb.state_offset != G->state_base[j] + (int64_t)ambient[j] * id) return kTable;
       if (pb.delta_offset != G->delta_base[j] + (int64_t)sizes[j] * id) return kTable;
     }
   // Slot-0 id range (the repacked table of the cooperative gather).
@@ -675,8 +725,8 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
   }
   G->slot0_lo = lo;
   G->slot0_count = (int64_t)hi - lo + 1;
-  G->slot0_stride = (k.s0 + 1) & ~1;
-  G->packed_stride = cse::PackedRowDoubles(k.s0);
+  G->slot0_stride = (sizes[0] + 1) & ~1;  // per-block slot-0 gradient contributions
+  G->packed_stride = cse::PackedRowDoubles(ambient[0]);
 #ifdef CSE_TUNING
   if (const char* e = getenv("CSE_TUNE_CAMSTRIDE")) G->packed_stride = std::max(G->slot0_stride, atoi(e));
 #endif
@@ -696,7 +746,7 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
     for (int j = 0; j < k.nb; ++j)
       for (int r = 0; r < k.nr; ++r)
         if (O[L[gidx(i)] + j * k.nr + r] != G->jac_base[j][r] + G->jac_stride[j] * i) return kTable;
-  const int N = k.s0 + k.s1;
+  const int N = sizes[0] + sizes[1];
   // Shape 1: packed cells (BlockSparseMatrix).
   bool packed = true;
   for (int j = 0; j < k.nb; ++j) {
@@ -843,20 +893,24 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
   cg.apply_loss = ev->opts.apply_loss_function;
   const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
   if (P.nchunks > 0) {
-    using K = cse::SnavelyKind;
-    switch (G.loss.kind) {
-      case CSE_LOSS_HUBER:
-        hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossHuber>), grid,
-                           dim3(cse::kBlockThreads), 0, s, cg);
-        break;
-      case CSE_LOSS_CAUCHY:
-        hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossCauchy>), grid,
-                           dim3(cse::kBlockThreads), 0, s, cg);
-        break;
-      default:
-        hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossTrivial>), grid,
-                           dim3(cse::kBlockThreads), 0, s, cg);
-    }
+    auto launch = [&](auto kd) {
+      using K = decltype(kd);
+      switch (G.loss.kind) {
+        case CSE_LOSS_HUBER:
+          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossHuber>), grid,
+                             dim3(cse::kBlockThreads), 0, s, cg);
+          break;
+        case CSE_LOSS_CAUCHY:
+          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossCauchy>), grid,
+                             dim3(cse::kBlockThreads), 0, s, cg);
+          break;
+        default:
+          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossTrivial>), grid,
+                             dim3(cse::kBlockThreads), 0, s, cg);
+      }
+    };
+    if (G.kind == kKindQuaternionTangent) launch(cse::SnavelyQuaternionTangentKind{});
+    else launch(cse::SnavelyKind{});
   }
   cse::GradArgs ga{};
   ga.count = P.count;
@@ -882,7 +936,7 @@ int BuildSchurPlan(cse_evaluator* ev, const cse_problem_desc* d, hipStream_t s) 
   S.eligible = false;
   if (ev->groups.size() != 1 || d->num_groups != 1) return CSE_OK;
   const Group& G = ev->groups[0];
-  if (!G.fuse_ok || G.policy != kAffinePacked || G.kind != CSE_FUNCTOR_SNAVELY_2_9_3 ||
+  if (!G.fuse_ok || G.policy != kAffinePacked || !FusedKind(G.kind) ||
       !ev->has_layout || ev->num_constant > 0)
     return CSE_OK;
   const cse_residual_group& g = d->groups[0];
@@ -987,14 +1041,14 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       a.gfused = d_grad;
       a.gside = G.gside.p;
       a.gcontrib = G.gcontrib.p;
-      fn = recompute ? PickFusedPoints(G.loss.kind, G.policy) : PickFused(G.loss.kind, G.policy);
+      fn = PickFused(G.kind, G.loss.kind, G.policy, recompute);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
-      const int pieces = (G.shape.s0 + 1) / 2;
+      const int pieces = (G.shape.x0 + 1) / 2;
       const int64_t total = G.slot0_count * pieces;
       hipLaunchKernelGGL(cse::RepackSlot0Kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                         ev->stream, d_state, G.state_base[0], G.shape.s0, G.packed_stride, pieces,
+                         ev->stream, d_state, G.state_base[0], G.shape.x0, G.packed_stride, pieces,
                          G.slot0_lo, G.slot0_count, G.packed0.p);
     }
     fn(a, G.num_wg, ev->stream);
@@ -1139,7 +1193,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   for (int gi = 0; gi < d->num_groups; ++gi) {
     const cse_residual_group& g = d->groups[gi];
     Group G;
-    if (!ShapeOf(g.functor_kind, &G.shape))
+    if (g.functor_kind < 0 || !ShapeOf(g.functor_kind, &G.shape))
       return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown functor kind " + std::to_string(g.functor_kind)));
     if (g.loss.kind < CSE_LOSS_TRIVIAL || g.loss.kind > CSE_LOSS_CAUCHY)
       return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown loss kind " + std::to_string(g.loss.kind)));
@@ -1202,6 +1256,13 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     ev->bytes_jac += per_block * g.num_blocks;
     G.policy = ev->opts.force_general_layout ? kTable : DetectAffine(d, g, k, &G);
     G.affine = G.policy != kTable;
+    if (G.affine && g.functor_kind == CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 &&
+        d->parameter_blocks[g.parameter_block_ids[0]].manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
+      // Slot 0 on the quaternion manifold (DetectAffine checked every
+      // block): the kernel kind with the tangent Jacobian (k follows G.shape).
+      G.kind = kKindQuaternionTangent;
+      ShapeOf(G.kind, &G.shape);
+    }
     if (!G.affine) ev->any_general = true;
     if (G.affine) {
       const int64_t chunks = (g.num_blocks + cse::kWave - 1) / cse::kWave;
@@ -1238,7 +1299,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   // and whose slot-0 blocks have a chunked plan.
   for (int gi = 0; gi < (int)ev->groups.size(); ++gi) {
     Group& G = ev->groups[gi];
-    bool ok = G.kind == CSE_FUNCTOR_SNAVELY_2_9_3 && G.affine && G.n > 0 && G.packed0.p &&
+    bool ok = FusedKind(G.kind) && G.affine && G.n > 0 && G.packed0.p &&
               G.grad[0].ready && G.grad[0].perm.p && G.grad[0].nchunks > 0 && G.grad[1].ready &&
               G.grad[1].perm.p == nullptr;
     const cse_residual_group& g = d->groups[gi];
@@ -1257,8 +1318,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     std::vector<cse::PbDev> pbs(d->num_parameter_blocks);
     for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
       const cse_parameter_block& pb = d->parameter_blocks[b];
-      pbs[b] = {pb.state_offset, pb.delta_offset, pb.plus_jacobian_offset, pb.tangent_size,
-                pb.is_constant};
+      const int64_t pj = pb.manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN
+                             ? cse::kPlusJacobianQuaternion
+                             : pb.plus_jacobian_offset;
+      pbs[b] = {pb.state_offset, pb.delta_offset, pj, pb.tangent_size, pb.is_constant};
     }
     if ((rc = ev->pbs.upload(pbs.data(), pbs.size(), s))) return bail(rc);
     if ((rc = ev->res_layout.upload(d->residual_layout, (size_t)d->num_residual_blocks, s))) return bail(rc);

@@ -122,7 +122,7 @@ __device__ __forceinline__ void AddGradientSlot(double* g, int t, const double* 
 template <class K>
 struct AffineInputs {
   double d[KindTraits<K>::D];
-  double x0[KindTraits<K>::S0];
+  double x0[KindTraits<K>::X0];  // ambient values
   double x1[KindTraits<K>::S1p];
   int32_t id0, id1;
 };
@@ -171,22 +171,22 @@ __device__ __forceinline__ void GatherDataAndSlot1(const GroupArgs& a, int64_t i
 template <class K>
 __device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 id,
                                            AffineInputs<K>* in, double* lds, int lane) {
-  constexpr int S0 = KindTraits<K>::S0;
+  constexpr int X0 = KindTraits<K>::X0;
   GatherDataAndSlot1<K, false>(a, i, id, in);
   const double* base0 = a.state + a.state_base[0];
-  double piece[S0];
+  double piece[X0];
 #pragma unroll
-  for (int k = 0; k < S0; ++k) {
+  for (int k = 0; k < X0; ++k) {
     const int p = k * kWave + lane;
-    const int t = p / S0, q = p - t * S0;
+    const int t = p / X0, q = p - t * X0;
     const int cid = __shfl(id.x, t, kWave);
-    piece[k] = base0[(int64_t)S0 * cid + q];
+    piece[k] = base0[(int64_t)X0 * cid + q];
   }
 #pragma unroll
-  for (int k = 0; k < S0; ++k) lds[k * kWave + lane] = piece[k];
+  for (int k = 0; k < X0; ++k) lds[k * kWave + lane] = piece[k];
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0 + k];
+  for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0 + k];
   __builtin_amdgcn_wave_barrier();
   in->id0 = id.x;
   in->id1 = id.y;
@@ -206,10 +206,10 @@ template <class K, int kStride = 0, bool kOwn = false>
 __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int2 id,
                                               AffineInputs<K>* in, double* lds, int lane) {
   using Tr = KindTraits<K>;
-  constexpr int S0 = Tr::S0;
-  constexpr int S0p = (S0 + 1) & ~1;  // doubles per block in the packed table
-  constexpr int kPieces = S0p / 2;    // 16-byte pieces per block
-  constexpr int kRow = kStride ? kStride : PackedRowDoubles(S0);
+  constexpr int X0 = Tr::X0;
+  constexpr int X0p = (X0 + 1) & ~1;  // doubles per block in the packed table
+  constexpr int kPieces = X0p / 2;    // 16-byte pieces per block
+  constexpr int kRow = kStride ? kStride : PackedRowDoubles(X0);
   const int cid_own = id.x - a.packed0_lo;
 #pragma unroll
   for (int k = 0; k < kPieces; ++k) {
@@ -229,10 +229,10 @@ __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int
   __builtin_amdgcn_wave_barrier();
   if constexpr (kOwn) {
 #pragma unroll
-    for (int k = 0; k < S0; ++k) in->x0[k] = lds[2 * kWave * (k / 2) + 2 * lane + (k & 1)];
+    for (int k = 0; k < X0; ++k) in->x0[k] = lds[2 * kWave * (k / 2) + 2 * lane + (k & 1)];
   } else {
 #pragma unroll
-    for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+    for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
   }
   __builtin_amdgcn_wave_barrier();
   in->id0 = id.x;
@@ -246,28 +246,28 @@ template <class K, bool kReg>
 __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 id,
                                             AffineInputs<K>* in, double* lds, int lane) {
   using Tr = KindTraits<K>;
-  constexpr int S0 = Tr::S0, S1 = Tr::S1, D = Tr::D;
-  constexpr int S0p = (S0 + 1) & ~1;
-  constexpr int kPieces = S0p / 2;
+  constexpr int X0 = Tr::X0, S1 = Tr::S1, D = Tr::D;
+  constexpr int X0p = (X0 + 1) & ~1;
+  constexpr int kPieces = X0p / 2;
   static_assert(D == 2, "observation pairs");
   const double obs_x = __builtin_nontemporal_load(a.data + 2 * i);
   const double obs_y = __builtin_nontemporal_load(a.data + 2 * i + 1);
   const int cid_own = id.x - a.packed0_lo;
   if constexpr (kReg) {
     const double2* src =
-        reinterpret_cast<const double2*>(a.packed0 + (int64_t)PackedRowDoubles(S0) * cid_own);
+        reinterpret_cast<const double2*>(a.packed0 + (int64_t)PackedRowDoubles(X0) * cid_own);
     double2 v[kPieces];
 #pragma unroll
     for (int k = 0; k < kPieces; ++k) v[k] = src[k];
 #pragma unroll
-    for (int k = 0; k < S0; ++k) in->x0[k] = (k & 1) ? v[k / 2].y : v[k / 2].x;
+    for (int k = 0; k < X0; ++k) in->x0[k] = (k & 1) ? v[k / 2].y : v[k / 2].x;
   } else {
 #pragma unroll
     for (int k = 0; k < kPieces; ++k) {
       const int p = k * kWave + lane;
       const int t = p / kPieces, q = p - t * kPieces;
       const int cid = __shfl(cid_own, t, kWave);
-      const double* src = a.packed0 + (int64_t)PackedRowDoubles(S0) * cid + 2 * q;
+      const double* src = a.packed0 + (int64_t)PackedRowDoubles(X0) * cid + 2 * q;
       __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
     }
   }
@@ -282,7 +282,7 @@ __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int k = 0; k < S0; ++k) in->x0[k] = lds[lane * S0p + k];
+    for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
     __builtin_amdgcn_wave_barrier();
   }
   in->id0 = id.x;
@@ -547,7 +547,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
                                         : kTwo ? NR * (S0 > S1 ? S0 : S1)
                                                : kLdsE ? NR * (S0 + S1) : NR * S0)
                                 : 1;
-  constexpr int kCoopLane = kCoop == 2 ? ((S0 + 1) & ~1) : S0;
+  constexpr int kCoopLane = kCoop == 2 ? ((Tr::X0 + 1) & ~1) : Tr::X0;
   // StageAndStore's footprint (ragged chunks): whole rows (CRS) or one
   // slot's cells at a time (BSM).
   constexpr int kSlowLane = !kJac ? 1 : kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N) : NR * (S0 > S1 ? S0 : S1);
@@ -586,7 +586,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       GatherDataAndSlot1<K, true>(a, i, id, &in);
       const double* row = a.packed0;
 #pragma unroll
-      for (int k = 0; k < S0; ++k) in.x0[k] = row[k];
+      for (int k = 0; k < Tr::X0; ++k) in.x0[k] = row[k];
       in.id0 = id.x;
       in.id1 = id.y;
     } else if constexpr (T::kEarlyObs || T::kRegGather ||
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksFusedPoi
 // block order, 5.8 GB of lines gathered back in camera order at
 // problem-13682, GradientContribKernel).  Here each wave takes one chunk of
 // at most kGradChunk consecutive entries of one camera's block list and
-// evaluates those blocks again with the camera's 9 partials only (Jet<S0>,
+// evaluates those blocks again with the camera's partials only (Jet<X0>,
 // the point a constant): the camera is uniform over the wave, the functor
 // data and point ids stream in camera order from a copy sorted once at
 // setup (SortSlot0InputsKernel), and only the 24-byte points are gathered
@@ -980,23 +980,28 @@ struct CamGradArgs {
 };
 
 // r and the slot-0 Jacobian (NR x S0, row-major) of one block, the slot-1
-// parameters held constant (AutoDifferentiate with only slot 0 seeded).
+// parameters held constant (AutoDifferentiate with only slot 0 seeded; a
+// slot-0 manifold maps the X0 ambient partials to the S0 tangent columns).
 template <class K>
 __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
                                               const double* x1, double* r, double* J0) {
   using Tr = KindTraits<K>;
-  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1;
-  Jet<S0> j0[S0], j1[S1], out[NR];
+  constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1;
+  Jet<X0> j0[X0], j1[S1], out[NR];
 #pragma unroll
-  for (int k = 0; k < S0; ++k) j0[k] = Jet<S0>(x0[k], k);
+  for (int k = 0; k < X0; ++k) j0[k] = Jet<X0>(x0[k], k);
 #pragma unroll
-  for (int k = 0; k < S1; ++k) j1[k] = Jet<S0>(x1[k]);
+  for (int k = 0; k < S1; ++k) j1[k] = Jet<X0>(x1[k]);
   K::Evaluate(d, j0, j1, out);
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     r[k] = out[k].a;
+    if constexpr (X0 == S0) {
 #pragma unroll
-    for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+      for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+    } else {
+      K::TangentRow(x0, out[k].v, J0 + k * S0);
+    }
   }
 }
 
@@ -1010,10 +1015,11 @@ __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamG
   const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (cid >= g.nchunks) return;
   const int64_t q0 = g.chunk_begin[cid], q1 = g.chunk_begin[cid + 1];
-  const double* cam = g.state + g.state_base0 + (int64_t)S0 * g.chunk_pb[cid];
-  double x0[S0];
+  constexpr int X0 = Tr::X0;
+  const double* cam = g.state + g.state_base0 + (int64_t)X0 * g.chunk_pb[cid];
+  double x0[X0];
 #pragma unroll
-  for (int k = 0; k < S0; ++k) x0[k] = cam[k];
+  for (int k = 0; k < X0; ++k) x0[k] = cam[k];
   double acc[S0];
 #pragma unroll
   for (int c = 0; c < S0; ++c) acc[c] = 0.0;
@@ -1135,9 +1141,37 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const Group
       // place: slot j keeps its tangent columns first.
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        if (pb[j].plus_jacobian_offset < 0) continue;
         constexpr int kMax = Tr::MaxSize();
         const int S = Tr::Size(j), o = Tr::Off(j);
+        if (pb[j].plus_jacobian_offset == kPlusJacobianQuaternion) {
+          // CSE_MANIFOLD_QUATERNION_EUCLIDEAN: the plus-Jacobian from the
+          // block's value (QuaternionEuclideanTangentRow), in place.
+          if constexpr (kMax >= 4) {
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+              double* row = J + k * N + o;
+              const double* q = x + o;
+              double L[3];
+              const double P[4][3] = {{-q[1], -q[2], -q[3]}, {q[0], q[3], -q[2]},
+                                      {-q[3], q[0], q[1]}, {q[2], -q[1], q[0]}};
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+                double s = 0.0;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) s += row[m] * P[m][c];
+                L[c] = s;
+              }
+#pragma unroll
+              for (int c = 3; c < kMax - 1; ++c)
+                if (c < S - 1) row[c] = row[c + 1];
+              row[0] = L[0];
+              row[1] = L[1];
+              row[2] = L[2];
+            }
+          }
+          continue;
+        }
+        if (pb[j].plus_jacobian_offset < 0) continue;
         const double* PJ = a.plus_jacobians + pb[j].plus_jacobian_offset;
         const int t = pb[j].tangent_size;
 #pragma unroll

@@ -220,6 +220,54 @@ struct SnavelyQuaternionKind {
   CSE_FLAT_FROM_TWO_SLOTS
 };
 
+// One row of an ambient Jacobian (kS columns) of a block on
+// ProductManifold<QuaternionManifold, EuclideanManifold<kS - 4>> times the
+// manifold's plus-Jacobian: the 4 x 3 QuaternionPlusJacobianImpl of
+// q = x[0..4) (internal/ceres/manifold.cc:62-78, Ceres order w, x, y, z)
+// and an identity for the Euclidean part, block-diagonal
+// (product_manifold.h).  out has kS - 1 columns.  Each sum adds the nonzero
+// terms in the order of the dense product (residual_block.cc:133-156), so
+// the result equals that product with the explicit matrix up to the sign of
+// zeros.
+template <int kS>
+CSE_HD void QuaternionEuclideanTangentRow(const double* x, const double* amb, double* out) {
+  static_assert(kS >= 4, "quaternion first");
+  const double w = x[0], qx = x[1], qy = x[2], qz = x[3];
+  const double P[4][3] = {{-qx, -qy, -qz}, {w, qz, -qy}, {-qz, w, qx}, {qy, -qx, w}};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double s = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) s += amb[m] * P[m][c];
+    out[c] = s;
+  }
+#pragma unroll
+  for (int c = 3; c < kS - 1; ++c) out[c] = amb[c + 1];
+}
+
+// SnavelyQuaternionKind with its camera on ProductManifold<QuaternionManifold,
+// EuclideanManifold<6>> (CSE_MANIFOLD_QUATERNION_EUCLIDEAN; the
+// --use_quaternions --use_manifolds problem of examples/bundle_adjuster.cc:
+// 337-345): the affine kernels gather the 10 ambient camera values
+// (kAmbient0) and write the 9 tangent Jacobian columns (kSize0), as the
+// 9-parameter Snavely camera.  Affine kernels only (no flat form).
+struct SnavelyQuaternionTangentKind {
+  static constexpr int kNumResiduals = 2;
+  static constexpr int kNumBlocks = 2;
+  static constexpr int kSize0 = 9, kSize1 = 3;
+  static constexpr int kAmbient0 = 10;
+  static constexpr int kSizes[2] = {9, 3};
+  static constexpr int kDataSize = 2;
+  static constexpr bool kAffineOnly = true;
+  template <typename T>
+  static CSE_HD bool Evaluate(const double* obs, const T* camera, const T* point, T* r) {
+    return SnavelyQuaternionKind::Evaluate(obs, camera, point, r);
+  }
+  static CSE_HD void TangentRow(const double* x0, const double* amb, double* out) {
+    QuaternionEuclideanTangentRow<10>(x0, amb, out);
+  }
+};
+
 // PointDisplacementError<3, 3> (internal/ceres/evaluator_cuda_test.cu.cc:84-110).
 struct PointDisplacementKind {
   static constexpr int kNumResiduals = 3;

@@ -24,7 +24,10 @@ constexpr int kMaxSlots = 10;  // parameter blocks per residual block (table pat
 // AutoDifferentiate pre-fills outputs with.
 constexpr double kImpossibleValue = 1e302;
 
-// Device copy of a parameter block (table path).
+// Device copy of a parameter block (table path).  plus_jacobian_offset:
+// >= 0 the explicit matrix, -1 none, kPlusJacobianQuaternion the
+// CSE_MANIFOLD_QUATERNION_EUCLIDEAN manifold (built in registers).
+constexpr int64_t kPlusJacobianQuaternion = -2;
 struct PbDev {
   int64_t state_offset;
   int64_t delta_offset;
@@ -92,11 +95,23 @@ constexpr int MaxSlotSize() {
   for (int b = 0; b < K::kNumBlocks; ++b) m = K::kSizes[b] > m ? K::kSizes[b] : m;
   return m;
 }
+// Values gathered for slot 0: K::kAmbient0 where the kind declares it (a
+// slot-0 manifold: kSize0 is then the tangent size, the Jacobian's
+// columns), else kSize0.
+template <class K, class = void>
+struct Ambient0 {
+  static constexpr int value = K::kSize0;
+};
+template <class K>
+struct Ambient0<K, decltype((void)K::kAmbient0)> {
+  static constexpr int value = K::kAmbient0;
+};
 template <class K>
 struct KindTraits {
   static constexpr int NR = K::kNumResiduals;
   static constexpr int NB = K::kNumBlocks;
-  static constexpr int S0 = K::kSize0;
+  static constexpr int S0 = K::kSize0;   // slot-0 Jacobian columns (tangent)
+  static constexpr int X0 = Ambient0<K>::value;  // slot-0 values (ambient)
   static constexpr int S1 = NB > 1 ? K::kSize1 : 0;
   static constexpr int S1p = S1 > 0 ? S1 : 1;
   static constexpr int D = K::kDataSize;
@@ -125,6 +140,17 @@ struct TestOnly {
 template <class K>
 struct TestOnly<K, decltype((void)K::kTestOnly)> {
   static constexpr bool value = K::kTestOnly;
+};
+
+// Does the kind run on the affine kernels only (no flat form for the
+// table kernel)?
+template <class K, class = void>
+struct AffineOnly {
+  static constexpr bool value = false;
+};
+template <class K>
+struct AffineOnly<K, decltype((void)K::kAffineOnly)> {
+  static constexpr bool value = K::kAffineOnly;
 };
 
 // Row stride (doubles) of the repacked slot-0 table that the LDS-DMA gather
@@ -232,23 +258,27 @@ template <class K, bool kJac>
 CSE_HD bool EvaluateFunctor(const double* d, const double* x0, const double* x1, double* r,
                             double* J0, double* J1) {
   using Tr = KindTraits<K>;
-  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = S0 + S1;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1, S1p = Tr::S1p, N = X0 + S1;
   if constexpr (kJac) {
-    Jet<N> j0[S0], j1[S1p], out[NR];
+    Jet<N> j0[X0], j1[S1p], out[NR];
 #pragma unroll
-    for (int k = 0; k < S0; ++k) j0[k] = Jet<N>(x0[k], k);
+    for (int k = 0; k < X0; ++k) j0[k] = Jet<N>(x0[k], k);
 #pragma unroll
-    for (int k = 0; k < S1; ++k) j1[k] = Jet<N>(x1[k], S0 + k);
+    for (int k = 0; k < S1; ++k) j1[k] = Jet<N>(x1[k], X0 + k);
 #pragma unroll
     for (int k = 0; k < NR; ++k) out[k] = Jet<N>::Filled(kImpossibleValue);
     const bool ok = K::Evaluate(d, j0, j1, out);
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       r[k] = out[k].a;
+      if constexpr (X0 == S0) {
 #pragma unroll
-      for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+        for (int c = 0; c < S0; ++c) J0[k * S0 + c] = out[k].v[c];
+      } else {  // slot-0 manifold: ambient row times the plus-Jacobian
+        K::TangentRow(x0, out[k].v, J0 + k * S0);
+      }
 #pragma unroll
-      for (int c = 0; c < S1; ++c) J1[k * S1p + c] = out[k].v[S0 + c];
+      for (int c = 0; c < S1; ++c) J1[k * S1p + c] = out[k].v[X0 + c];
     }
     return ok;
   } else {

@@ -28,6 +28,7 @@
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -121,6 +122,9 @@ class Manifold {
   virtual int AmbientSize() const = 0;
   virtual int TangentSize() const = 0;
   virtual void PlusJacobian(const double* x, double* jacobian) const = 0;
+  // cse_manifold_kind the library can build on the device from the block's
+  // value; CSE_MANIFOLD_MATRIX = upload PlusJacobian every evaluation.
+  virtual int DeviceKind() const { return CSE_MANIFOLD_MATRIX; }
 };
 
 template <int N>
@@ -168,10 +172,22 @@ class SubsetManifold : public Manifold {
   std::vector<int> keep_;
 };
 
+template <typename M>
+struct IsEuclideanManifold : std::false_type {};
+template <int N>
+struct IsEuclideanManifold<EuclideanManifold<N>> : std::true_type {};
+
 // ProductManifold<M1, M2>: block-diagonal plus-Jacobian.
 template <typename M1, typename M2>
 class ProductManifold : public Manifold {
  public:
+  // ProductManifold<QuaternionManifold, EuclideanManifold<n>> (the
+  // --use_quaternions --use_manifolds camera): built on the device.
+  int DeviceKind() const override {
+    return std::is_same<M1, QuaternionManifold>::value && IsEuclideanManifold<M2>::value
+               ? CSE_MANIFOLD_QUATERNION_EUCLIDEAN
+               : CSE_MANIFOLD_MATRIX;
+  }
   int AmbientSize() const override { return m1_.AmbientSize() + m2_.AmbientSize(); }
   int TangentSize() const override { return m1_.TangentSize() + m2_.TangentSize(); }
   void PlusJacobian(const double* x, double* J) const override {
@@ -332,6 +348,9 @@ class EvaluatorCUDA {
     int device = -1;
     bool check_finite = true;
     bool apply_loss_function = true;
+    // Let the library build the plus-Jacobians it knows (Manifold::DeviceKind)
+    // instead of uploading them every evaluation.
+    bool device_manifolds = true;
   };
 
   EvaluatorCUDA(ProblemCUDA& problem, const Options& options) : problem_(problem) {
@@ -413,7 +432,7 @@ class EvaluatorCUDA {
       b.size = p.size;
       b.tangent_size = p.manifold ? p.manifold->TangentSize() : p.size;
       b.is_constant = p.constant;
-      b.reserved = 0;
+      b.manifold = p.manifold && o.device_manifolds ? p.manifold->DeviceKind() : CSE_MANIFOLD_MATRIX;
       b.plus_jacobian_offset = -1;
       if (p.constant) {
         b.state_offset = cso;
@@ -425,7 +444,7 @@ class EvaluatorCUDA {
         b.delta_offset = dof;
         so += p.size;
         dof += b.tangent_size;
-        if (p.manifold) {
+        if (p.manifold && b.manifold == CSE_MANIFOLD_MATRIX) {
           b.plus_jacobian_offset = num_plus_jacobian_values_;
           num_plus_jacobian_values_ += (int64_t)p.size * b.tangent_size;
         }
@@ -536,7 +555,7 @@ class EvaluatorCUDA {
   void RefreshPlusJacobians(const double* state) {
     for (size_t k = 0; k < order_.size(); ++k) {
       const auto& p = problem_.params_[order_[k]];
-      if (p.constant || !p.manifold) continue;
+      if (p.constant || !p.manifold || pbs_[k].plus_jacobian_offset < 0) continue;
       p.manifold->PlusJacobian(state + state_offset_[k],
                                plus_jacobians_.data() + pbs_[k].plus_jacobian_offset);
     }

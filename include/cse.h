@@ -99,11 +99,31 @@ typedef struct cse_parameter_block {
   int32_t size;                 /* ambient size */
   int32_t tangent_size;         /* == size without a manifold */
   int32_t is_constant;          /* held constant: no Jacobian, no gradient */
-  int32_t reserved;
+  int32_t manifold;             /* cse_manifold_kind */
   int64_t state_offset;         /* into state (active) / constant_state (constant) */
   int64_t delta_offset;         /* into the gradient (active only) */
   int64_t plus_jacobian_offset; /* into plus_jacobians (size x tangent row-major), -1 = none */
 } cse_parameter_block;
+
+/* How the evaluator gets a block's plus-Jacobian (Manifold::PlusJacobian).
+ *   CSE_MANIFOLD_MATRIX: the size x tangent_size matrix at
+ *       plus_jacobian_offset, refreshed by cse_set_plus_jacobians, as the
+ *       reference uploads it (registered_cuda_evaluators.cc:139-160);
+ *       plus_jacobian_offset -1 = no manifold.
+ *   CSE_MANIFOLD_QUATERNION_EUCLIDEAN: ProductManifold<QuaternionManifold,
+ *       EuclideanManifold<size - 4>> (Ceres order w, x, y, z first; the
+ *       --use_quaternions --use_manifolds camera of examples/bundle_adjuster.cc:
+ *       337-345 and evaluator_cuda_test.cu.cc:286): tangent_size = size - 1,
+ *       plus_jacobian_offset must be -1.  The kernels build the plus-Jacobian
+ *       (QuaternionPlusJacobianImpl, internal/ceres/manifold.cc:62-78, and an
+ *       identity block) from the block's current value in registers; the
+ *       result equals the dense product with that matrix.  Blocks of this kind
+ *       in slot 0 of SNAVELY_QUATERNION_2_10_3 groups keep the affine (fast)
+ *       kernels; Plus on device is not available for them. */
+typedef enum cse_manifold_kind {
+  CSE_MANIFOLD_MATRIX = 0,
+  CSE_MANIFOLD_QUATERNION_EUCLIDEAN = 1
+} cse_manifold_kind;
 
 /* All residual blocks of one (functor kind, loss) type; replaces one
  * AutoDiffResidualBlockCUDAEvaluator<F, Loss, kR, Ns...> and its residual

@@ -109,6 +109,10 @@ class OracleProgram:
 
     @classmethod
     def from_program(cls, prog, apply_loss_function=True):
+        # The reference's form: every manifold as its explicit plus-Jacobian
+        # (Program.with_explicit_manifolds, at the Program's state).
+        if getattr(prog, "pb_manifold", None) is not None and np.any(prog.pb_manifold):
+            raise ValueError("OracleProgram: convert with prog.with_explicit_manifolds(state) first")
         nrb = prog.num_residual_blocks
         kind = np.zeros(nrb, np.int32)
         lk = np.zeros(nrb, np.int32)

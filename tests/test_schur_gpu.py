@@ -63,12 +63,15 @@ def close(a, b, tol=RTOL):
     return np.linalg.norm(a - b) <= tol * max(np.linalg.norm(b), 1e-300)
 
 
-@pytest.mark.parametrize("which", ["bal", "runs"])
+@pytest.mark.parametrize("which", ["bal", "runs", "quaternion"])
 @pytest.mark.parametrize("precond", [_cse.SCHUR_IDENTITY, _cse.SCHUR_JACOBI,
                                      _cse.SCHUR_SCHUR_JACOBI])
 def test_schur_operators_match_dense(gpu, which, precond):
-    prog = (bal.synthetic_program((10, 300, 1500), loss=ca.Loss.huber(1.0), seed=9)
-            if which == "bal" else runs_problem())
+    # quaternion: cameras on ProductManifold<QuaternionManifold, EuclideanManifold<6>>
+    # (9 tangent columns per f block, as the angle-axis camera).
+    prog = (runs_problem() if which == "runs" else
+            bal.synthetic_program((10, 300, 1500), loss=ca.Loss.huber(1.0), seed=9,
+                                  quaternion_manifold=which == "quaternion"))
     dev = torch.device("cuda", 0)
     ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
     ok, cost, r, g, jv = ev.evaluate()
