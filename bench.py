@@ -87,6 +87,9 @@ def parse():
                          "SnavelyReprojectionErrorWithQuaternions<2,10,3> with every camera on "
                          "ProductManifold<QuaternionManifold, EuclideanManifold<6>> "
                          "(bundle_adjuster --use_quaternions --use_manifolds)")
+    ap.add_argument("--held-cameras", type=int, default=0,
+                    help="hold the first K cameras constant (SetParameterBlockConstant, e.g. the "
+                         "gauge): their blocks have no F cell (BlockSparseMatrix); not the headline")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the gradient / residual-only / host-strip legs")
     ap.add_argument("--secondary-steps", type=int, default=20)
@@ -278,9 +281,11 @@ def main():
     se = distributed.ShardedEvaluator(*arrays, srank, sworld, device=dev_index,
                                       loss=make_loss(args.loss), format=args.format,
                                       gradient=True, gradient_mode=args.gradient_mode,
-                                      stream=stream, quaternion_manifold=quat)
+                                      stream=stream, quaternion_manifold=quat,
+                                      constant_cameras=tuple(range(args.held_cameras)))
+    variant = quat or args.held_cameras > 0
     if not (rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "jacobian"
-            and not quat):
+            and not variant):
         del arrays
         arrays = None
     build_s = time.perf_counter() - t_build
@@ -479,16 +484,18 @@ def main():
             cpu = cpu_baseline(args, arrays, threads)
         traffic = None
         pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}_{args.loss}_{args.format}.json")
-        if (world == 1 and args.mode == "jacobian" and not args.gradient and not quat
+        if (world == 1 and args.mode == "jacobian" and not args.gradient and not variant
                 and os.path.exists(pmc_path)):
             with open(pmc_path) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         C_, P_, O_ = counts
         sh = se.shard
         out = {
-            "metric": METRIC if args.mode == "jacobian" and not quat else
+            "metric": METRIC if args.mode == "jacobian" and not variant else
                       f"{args.mode} evaluations/sec on BAL {args.config}"
-                      f"{' with quaternion cameras on their manifold' if quat else ''} (not the headline)",
+                      f"{' with quaternion cameras on their manifold' if quat else ''}"
+                      f"{f' with {args.held_cameras} held camera(s)' if args.held_cameras else ''}"
+                      " (not the headline)",
             "value": value,
             "unit": "evals/s",
             "n_gpus": world,
@@ -505,6 +512,7 @@ def main():
                             + ("SnavelyReprojectionErrorWithQuaternions<2,10,3>, cameras on "
                                "ProductManifold<QuaternionManifold, EuclideanManifold<6>> "
                                if quat else "SnavelyReprojectionError<2,9,3> ")
+                            + (f"{args.held_cameras} camera(s) held constant, " if args.held_cameras else "")
                             + f"{args.loss} {args.format} "
                             + {"jacobian": "residual+Jacobian", "residual": "residual+cost",
                                "candidate": "Plus + cost-only",

@@ -290,14 +290,16 @@ def to_quaternion_cameras(cameras):
 
 
 def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=None,
-            format=BLOCK_SPARSE, compile=True, quaternion_manifold=False):
+            format=BLOCK_SPARSE, compile=True, quaternion_manifold=False, constant_cameras=()):
     """The Schur-ordered Program of a BAL problem (observations must
     already be point-major, as synthetic() returns and
     schur_residual_order() produces).  10-parameter (quaternion) cameras
     take SNAVELY_QUATERNION_2_10_3; quaternion_manifold puts each on
     ProductManifold<QuaternionManifold, EuclideanManifold<6>>, as
     bundle_adjuster --use_quaternions --use_manifolds does
-    (examples/bundle_adjuster.cc:337-345)."""
+    (examples/bundle_adjuster.cc:337-345).  constant_cameras: camera indices
+    held constant (Problem::SetParameterBlockConstant, e.g. to fix the gauge):
+    their values move to the constant state and they get no delta columns."""
     if kind is None:
         kind = _cse.SNAVELY_QUATERNION_2_10_3 if cameras.shape[1] == 10 else _cse.SNAVELY_2_9_3
     C, P = cameras.shape[0], points.shape[0]
@@ -311,9 +313,18 @@ def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=None,
     ids[:, 1] = pt_idx
     group = ResidualGroup(kind, loss or Loss.trivial(), ids, np.ascontiguousarray(obs, np.float64),
                           None, 0)
-    state = np.concatenate([points.ravel(), cameras.ravel()])
-    prog = Program(pb_size, pb_size.copy(), np.zeros(npb, np.int32), np.full(npb, -1, np.int64),
-                   np.zeros(0), [group], len(cam_idx), state, np.zeros(0))
+    const = np.zeros(npb, np.int32)
+    cstate = np.zeros(0)
+    if len(constant_cameras):
+        cc = np.zeros(C, bool)
+        cc[np.asarray(constant_cameras, np.int64)] = True
+        const[P:] = cc
+        state = np.concatenate([points.ravel(), cameras[~cc].ravel()])
+        cstate = np.ascontiguousarray(cameras[cc].ravel(), np.float64)
+    else:
+        state = np.concatenate([points.ravel(), cameras.ravel()])
+    prog = Program(pb_size, pb_size.copy(), const, np.full(npb, -1, np.int64),
+                   np.zeros(0), [group], len(cam_idx), state, cstate)
     if quaternion_manifold:
         assert cam_size == 10, "quaternion cameras"
         prog.pb_manifold = np.zeros(npb, np.int32)
@@ -325,7 +336,8 @@ def program(cameras, points, cam_idx, pt_idx, obs, loss=None, kind=None,
 
 
 def synthetic_program(name_or_counts, loss=None, format=BLOCK_SPARSE, seed=0xCE2E5,
-                      compile=True, quaternion=False, quaternion_manifold=False):
+                      compile=True, quaternion=False, quaternion_manifold=False,
+                      constant_cameras=()):
     """A synthetic BAL Program; quaternion: 10-parameter cameras
     (to_quaternion_cameras), optionally on the quaternion manifold."""
     counts = CONFIGS[name_or_counts] if isinstance(name_or_counts, str) else name_or_counts
@@ -333,4 +345,4 @@ def synthetic_program(name_or_counts, loss=None, format=BLOCK_SPARSE, seed=0xCE2
     if quaternion or quaternion_manifold:
         cams = to_quaternion_cameras(cams)
     return program(cams, pts, ci, pi, obs, loss=loss, format=format, compile=compile,
-                   quaternion_manifold=quaternion_manifold)
+                   quaternion_manifold=quaternion_manifold, constant_cameras=constant_cameras)

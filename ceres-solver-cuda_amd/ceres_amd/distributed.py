@@ -34,18 +34,21 @@ class ShardedEvaluator:
 
     def __init__(self, cameras, points, cam_idx, pt_idx, obs, rank, world, device, loss=None,
                  format=BLOCK_SPARSE, gradient=False, gradient_mode=0, stream=None, group=None,
-                 quaternion_manifold=False):
+                 quaternion_manifold=False, constant_cameras=()):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
         self.rank, self.world = rank, world
         self.num_points, self.num_cameras = points.shape[0], cameras.shape[0]
+        # gradient rows: the active cameras only
+        self.num_cameras -= len(set(int(c) for c in constant_cameras))
         # camera gradient rows: the tangent size (9 for the quaternion camera
         # on its manifold)
         self.cam_size = cameras.shape[1] - (1 if quaternion_manifold else 0)
         self.program, self.shard = _shard.shard_program(cameras, points, cam_idx, pt_idx, obs,
                                                         rank, world, loss=loss, format=format,
-                                                        quaternion_manifold=quaternion_manifold)
+                                                        quaternion_manifold=quaternion_manifold,
+                                                        constant_cameras=constant_cameras)
         self.device = torch.device("cuda", device)
         if stream is None:
             stream = torch.cuda.current_stream(self.device)

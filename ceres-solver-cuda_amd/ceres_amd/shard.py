@@ -70,6 +70,9 @@ class Shard:
     blocks: tuple     # [b0, b1)
     num_observations: int
     format: str
+    # Held (constant) cameras, BlockSparseMatrix: F cells exist only for the
+    # blocks of active cameras -- (cells before b0, cells in the shard).
+    f_cells: tuple = None
 
     @property
     def residual_strip(self):
@@ -84,7 +87,10 @@ class Shard:
         O = self.num_observations
         if self.format == BLOCK_SPARSE:
             e, f = nres * pt_size, nres * cam_size
-            return [(0, e * b0, e * n), (e * n, e * O + f * b0, f * n)]
+            f0, fn = self.f_cells if self.f_cells is not None else (b0, n)
+            return [(0, e * b0, e * n), (e * n, e * O + f * f0, f * fn)]
+        if self.f_cells is not None:
+            raise NotImplementedError("held cameras: BlockSparseMatrix strips only")
         w = nres * (cam_size + pt_size)
         return [(0, w * b0, w * n)]
 
@@ -99,15 +105,21 @@ def gradient_maps(shard, num_points, num_cameras, cam_size=9, pt_size=3):
 
 
 def shard_program(cameras, points, cam_idx, pt_idx, obs, rank, world, loss=None,
-                  format=BLOCK_SPARSE, compile=True, quaternion_manifold=False):
+                  format=BLOCK_SPARSE, compile=True, quaternion_manifold=False,
+                  constant_cameras=()):
     """The rank's Program: its points (renumbered from 0), every camera, its
     observations; same functor, loss and camera manifold as the full problem."""
     pc, bc = point_bucket_cuts(pt_idx, points.shape[0], world)
     p0, p1, b0, b1 = pc[rank], pc[rank + 1], bc[rank], bc[rank + 1]
     prog = bal.program(cameras, points[p0:p1], cam_idx[b0:b1],
                        np.asarray(pt_idx[b0:b1]) - p0, obs[b0:b1], loss=loss, format=format,
-                       compile=compile, quaternion_manifold=quaternion_manifold)
-    return prog, Shard(rank, world, (p0, p1), (b0, b1), len(cam_idx), format)
+                       compile=compile, quaternion_manifold=quaternion_manifold,
+                       constant_cameras=constant_cameras)
+    f_cells = None
+    if len(constant_cameras):
+        active = ~np.isin(np.asarray(cam_idx), np.asarray(constant_cameras))
+        f_cells = (int(active[:b0].sum()), int(active[b0:b1].sum()))
+    return prog, Shard(rank, world, (p0, p1), (b0, b1), len(cam_idx), format, f_cells)
 
 
 def assemble(shards, locals_, total):

@@ -196,7 +196,16 @@ struct Group {
     DevBuf<int32_t> chunk_pb;  // parameter block (id) of each chunk
     DevBuf<double> chunk_partial;
     int64_t nchunks = 0;
+    int64_t nperm = 0;  // blocks in the plan (all but those with a constant block)
   } grad[2];
+  // Constant slot-0 blocks on the affine path (BlockSparseMatrix): the
+  // active-bit table over the slot-0 id range, each id's repack source
+  // (state offset, or -1 - constant-state offset), and per 64-block chunk
+  // the offset of its first F cell.
+  bool const0 = false;
+  DevBuf<uint32_t> act0;
+  DevBuf<int64_t> src0, fbase, delta0;
+  std::vector<int64_t> h_fbase;
   // Fused gradient (cse::FusedGrad): eligible groups, and their slot-1
   // boundary entries and slot-0 contributions (allocated on first use).
   bool fuse_ok = false;
@@ -234,9 +243,9 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 // The shipped BSM Jacobian kernel of two-slot kinds (4 waves per SIMD).
-template <class K, int L, int Co>
+template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRound<K, L, Co>), dim3((unsigned)num_wg),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRound<K, L, Co, T>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
@@ -275,14 +284,14 @@ void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 // The affine kernel with the fused gradient (Snavely groups): with the
 // slot-0 contributions (gradient_mode 3) or points only (gradient_mode 0,
 // slot 0 from CameraGradientKernel).
-template <class K, int L, bool Crs>
+template <class K, int L, bool Crs, class T = cse::ShippedTune>
 void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<K, L, Crs>), dim3((unsigned)num_wg),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<K, L, Crs, T>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }
-template <class K, int L, bool Crs>
+template <class K, int L, bool Crs, class T = cse::PointsOnlyTune>
 void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs>), dim3((unsigned)num_wg),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs, T>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }
 
@@ -307,10 +316,30 @@ LaunchFn PickFusedK(int loss, bool crs, bool points) {
   }
 }
 
+template <class K>
+LaunchFn PickFusedC0(int loss, bool points) {
+  using TP = cse::PointsOnlyTuneC0;
+  using TF = cse::ShippedTuneC0;
+  switch (loss) {
+    case CSE_LOSS_HUBER:
+      return points ? &LaunchFusedPoints<K, cse::kLossHuber, false, TP> : &LaunchFused<K, cse::kLossHuber, false, TF>;
+    case CSE_LOSS_CAUCHY:
+      return points ? &LaunchFusedPoints<K, cse::kLossCauchy, false, TP> : &LaunchFused<K, cse::kLossCauchy, false, TF>;
+    default:
+      return points ? &LaunchFusedPoints<K, cse::kLossTrivial, false, TP> : &LaunchFused<K, cse::kLossTrivial, false, TF>;
+  }
+}
+
 // points = true: the slot-1 rows only (gradient_mode 0, slot 0 from
 // CameraGradientKernel); false: with the slot-0 contributions (mode 3).
-LaunchFn PickFused(int kind, int loss, int policy, bool points) {
+// const0: groups with constant slot-0 blocks (BSM).
+LaunchFn PickFused(int kind, int loss, int policy, bool points, bool const0 = false) {
   const bool crs = policy == kAffineCrs;
+  if (const0) {
+    if (crs) return nullptr;
+    if (kind == kKindQuaternionTangent) return PickFusedC0<cse::SnavelyQuaternionTangentKind>(loss, points);
+    return PickFusedC0<cse::SnavelyKind>(loss, points);
+  }
   if (kind == kKindQuaternionTangent)
     return PickFusedK<cse::SnavelyQuaternionTangentKind>(loss, crs, points);
   return PickFusedK<cse::SnavelyKind>(loss, crs, points);
@@ -439,10 +468,29 @@ LaunchFn TuningPick(int kind, int loss, bool jac, int policy, bool dma) {
 }
 #endif
 
-LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma) {
+// const0: the group has constant slot-0 blocks (FusedKind kinds, BSM, the
+// repacked table; DetectAffine): the Jacobian kernel with the packed F cells.
+LaunchFn PickConst0(int kind, int loss, bool jac) {
+  auto pick = [&](auto kd) -> LaunchFn {
+    using K = decltype(kd);
+    if (!jac) return nullptr;  // residual/cost kernels write no F cells: the usual ones
+    switch (loss) {
+      case CSE_LOSS_HUBER: return &LaunchTwoRound<K, cse::kLossHuber, 2, cse::ShippedTuneC0>;
+      case CSE_LOSS_CAUCHY: return &LaunchTwoRound<K, cse::kLossCauchy, 2, cse::ShippedTuneC0>;
+      default: return &LaunchTwoRound<K, cse::kLossTrivial, 2, cse::ShippedTuneC0>;
+    }
+  };
+  if (kind == kKindQuaternionTangent) return pick(cse::SnavelyQuaternionTangentKind{});
+  if (kind == CSE_FUNCTOR_SNAVELY_2_9_3) return pick(cse::SnavelyKind{});
+  return nullptr;
+}
+
+LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma, bool const0 = false) {
 #ifdef CSE_TUNING
-  if (LaunchFn f = TuningPick(kind, loss, jac, policy, dma)) return f;
+  if (!const0)
+    if (LaunchFn f = TuningPick(kind, loss, jac, policy, dma)) return f;
 #endif
+  if (const0 && jac) return policy == kAffinePacked && dma ? PickConst0(kind, loss, jac) : nullptr;
   LaunchFn fn = nullptr;
   VisitKind(kind, [&](auto kd) {
     using K = decltype(kd);
@@ -584,9 +632,15 @@ int Validate(const cse_problem_desc* d) {
 // for the two affine shapes).
 // Blocks of slot j listed per parameter block (stable counting sort): the
 // gradient post-pass sums each parameter block's blocks in this order.
+// cpb (may be null): the descriptor's parameter blocks; blocks whose slot-j
+// parameter block is constant are left out (a held camera has no gradient
+// row), which makes the plan a permutation of the other blocks only.
 int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group::GradPlan* plan,
-                  hipStream_t s) {
+                  hipStream_t s, const cse_parameter_block* cpb = nullptr) {
   const int64_t n = g.num_blocks;
+  auto skip = [&](int64_t i) {
+    return cpb && cpb[g.parameter_block_ids[i * k.nb + j]].is_constant;
+  };
   int32_t lo = g.parameter_block_ids[j], hi = lo;
   for (int64_t i = 0; i < n; ++i) {
     lo = std::min(lo, g.parameter_block_ids[i * k.nb + j]);
@@ -595,17 +649,26 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
   const int64_t count = (int64_t)hi - lo + 1;
   std::vector<int64_t> off(count + 1, 0);
   bool sorted = true;
+  int64_t kept = 0, prev = INT64_MIN;
   for (int64_t i = 0; i < n; ++i) {
+    if (skip(i)) {
+      sorted = false;  // a permutation of the kept blocks, never the identity
+      continue;
+    }
     const int32_t id = g.parameter_block_ids[i * k.nb + j];
     ++off[id - lo + 1];
-    if (i > 0 && id < g.parameter_block_ids[(i - 1) * k.nb + j]) sorted = false;
+    if (id < prev) sorted = false;
+    prev = id;
+    ++kept;
   }
+  plan->nperm = kept;
   for (int64_t p = 0; p < count; ++p) off[p + 1] += off[p];
   int rc;
   if (!sorted) {
-    std::vector<int32_t> perm(n);
+    std::vector<int32_t> perm(std::max<int64_t>(kept, 1));
     std::vector<int64_t> next(off.begin(), off.end() - 1);
-    for (int64_t i = 0; i < n; ++i) perm[next[g.parameter_block_ids[i * k.nb + j] - lo]++] = (int32_t)i;
+    for (int64_t i = 0; i < n; ++i)
+      if (!skip(i)) perm[next[g.parameter_block_ids[i * k.nb + j] - lo]++] = (int32_t)i;
     if ((rc = plan->perm.upload(perm.data(), perm.size(), s))) return rc;
     if (hipStreamSynchronize(s) != hipSuccess) return Fail(CSE_ERR_HIP, "hipStreamSynchronize failed");
   }
@@ -629,7 +692,7 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
     plan->nchunks = (int64_t)begin.size();
     // Chunk c covers [begin[c], begin[c + 1]): a parameter block's last
     // chunk ends at off[p + 1], where the next non-empty one starts.
-    begin.push_back(n);
+    begin.push_back(kept);
     if ((rc = plan->chunk_begin.upload(begin.data(), begin.size(), s))) return rc;
     if ((rc = plan->chunk_off.upload(coff.data(), coff.size(), s))) return rc;
     if (!cpb.empty() && (rc = plan->chunk_pb.upload(cpb.data(), cpb.size(), s))) return rc;
@@ -694,26 +757,51 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
   const int ambient[2] = {k.s0, k.s1};
   int sizes[2] = {k.s0, k.s1};
   int manifold[2] = {CSE_MANIFOLD_MATRIX, CSE_MANIFOLD_MATRIX};
+  // The first block whose slot j is active (bases and the manifold come from it).
+  int64_t first[2] = {-1, -1};
+  for (int64_t i = 0; i < n && (first[0] < 0 || (k.nb > 1 && first[1] < 0)); ++i)
+    for (int j = 0; j < k.nb; ++j)
+      if (first[j] < 0 && !d->parameter_blocks[g.parameter_block_ids[i * k.nb + j]].is_constant)
+        first[j] = i;
+  for (int j = 0; j < k.nb; ++j)
+    if (first[j] < 0) return kTable;
   if (g.functor_kind == CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 &&
-      d->parameter_blocks[g.parameter_block_ids[0]].manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
+      d->parameter_blocks[g.parameter_block_ids[first[0] * k.nb]].manifold ==
+          CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
     manifold[0] = CSE_MANIFOLD_QUATERNION_EUCLIDEAN;
     sizes[0] = k.s0 - 1;
   }
-  // Parameters: active, no explicit plus-Jacobian, state/delta offsets
-  // affine in the id.
+  // Constant slot-0 blocks (a held camera) are allowed for the kinds with the
+  // constant-aware kernels (the 9-column cameras, cse::ShippedTuneC0).
+  const bool const0_ok = k.nb == 2 && (g.functor_kind == CSE_FUNCTOR_SNAVELY_2_9_3 ||
+                                       manifold[0] == CSE_MANIFOLD_QUATERNION_EUCLIDEAN);
+  // Parameters: active (slot 0 may be constant, above), no explicit
+  // plus-Jacobian, state/delta offsets affine in the id.
   for (int j = 0; j < k.nb; ++j) {
-    const int32_t id0 = g.parameter_block_ids[j];
+    const int32_t id0 = g.parameter_block_ids[first[j] * k.nb + j];
     const cse_parameter_block& pb0 = d->parameter_blocks[id0];
     G->state_base[j] = pb0.state_offset - (int64_t)ambient[j] * id0;
     G->delta_base[j] = pb0.delta_offset - (int64_t)sizes[j] * id0;
   }
+  // With constant slot-0 blocks the active ones need not be affine either
+  // (a held camera in the middle shifts the later ones' offsets): their values
+  // come through the repacked table, their gradient rows through a table.
+  G->const0 = false;
+  for (int64_t i = 0; i < n && !G->const0; ++i)
+    G->const0 = d->parameter_blocks[g.parameter_block_ids[i * k.nb]].is_constant != 0;
+  if (G->const0 && !const0_ok) return kTable;
   for (int64_t i = 0; i < n; ++i)
     for (int j = 0; j < k.nb; ++j) {
       const int32_t id = g.parameter_block_ids[i * k.nb + j];
       const cse_parameter_block& pb = d->parameter_blocks[id];
-      if (pb.is_constant || pb.plus_jacobian_offset >= 0 || pb.manifold != manifold[j] ||
+      if (pb.is_constant) {
+        if (j != 0 || pb.size != ambient[0]) return kTable;
+        continue;
+      }
+      if (pb.plus_jacobian_offset >= 0 || pb.manifold != manifold[j] ||
           pb.tangent_size != sizes[j] || pb.size != ambient[j])
         return kTable;
+      if (j == 0 && G->const0) continue;
       if (pb.state_offset != G->state_base[j] + (int64_t)ambient[j] * id) return kTable;
       if (pb.delta_offset != G->delta_base[j] + (int64_t)sizes[j] * id) return kTable;
     }
@@ -738,6 +826,42 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
   if (!d->jacobian_per_residual_layout || !d->jacobian_per_residual_offsets) return kAffinePacked;
   const int64_t* L = d->jacobian_per_residual_layout;
   const int64_t* O = d->jacobian_per_residual_offsets;
+  if (G->const0) {
+    // BlockSparseMatrix only: the E (slot 1) cells affine, kR x S1 packed at
+    // e0 + kR*S1*i; the F cells of the blocks with an active camera packed in
+    // block order from f0 (a constant camera has none; its block's first
+    // active entries are the E rows).
+    const int NR = k.nr, S0 = sizes[0], S1 = sizes[1];
+    const int64_t f0 = O[L[gidx(first[0])]];
+    auto act = [&](int64_t i) {
+      return !d->parameter_blocks[g.parameter_block_ids[i * k.nb]].is_constant;
+    };
+    const int64_t e0 = O[L[gidx(0)] + (act(0) ? NR : 0)];
+    std::vector<int64_t> fb;
+    fb.reserve((size_t)((n + cse::kWave - 1) / cse::kWave));
+    int64_t rank = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      if (i % cse::kWave == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
+      const int64_t base = L[gidx(i)];
+      int a = 0;
+      if (act(i)) {
+        for (int r = 0; r < NR; ++r)
+          if (O[base + r] != f0 + (int64_t)NR * S0 * rank + (int64_t)r * S0) return kTable;
+        ++rank;
+        a = 1;
+      }
+      for (int r = 0; r < NR; ++r)
+        if (O[base + a * NR + r] != e0 + (int64_t)NR * S1 * i + (int64_t)r * S1) return kTable;
+    }
+    for (int r = 0; r < NR; ++r) {
+      G->jac_base[0][r] = f0 + (int64_t)r * S0;
+      G->jac_base[1][r] = e0 + (int64_t)r * S1;
+    }
+    G->jac_stride[0] = (int64_t)NR * S0;
+    G->jac_stride[1] = (int64_t)NR * S1;
+    G->h_fbase = std::move(fb);
+    return kAffinePacked;
+  }
   for (int j = 0; j < k.nb; ++j)
     for (int r = 0; r < k.nr; ++r) G->jac_base[j][r] = O[L[gidx(0)] + j * k.nr + r];
   for (int j = 0; j < k.nb; ++j)
@@ -795,6 +919,9 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.packed0 = G.packed0.p;
   a.packed0_lo = G.slot0_lo;
   a.packed0_stride = G.packed_stride;
+  a.act0_bits = G.act0.p;
+  a.fbase = G.fbase.p;
+  a.delta0 = G.delta0.p;
   a.gindex = G.gindex.p;
   a.first = G.first;
   a.residual_layout = ev->res_layout.p;
@@ -842,6 +969,7 @@ int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
   ga.lo = P.lo;
   ga.grad = out;
   ga.delta_base = G.delta_base[0];
+  ga.delta_tab = G.const0 ? G.delta0.p + (P.lo - G.slot0_lo) : nullptr;
   const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
   if (P.nchunks > 0)
     hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
@@ -868,7 +996,7 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
     if ((rc = G.sid1.alloc((size_t)G.n))) return rc;
     hipLaunchKernelGGL((cse::SortSlot0InputsKernel<2>),
                        dim3((unsigned)((G.n + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                       dim3(cse::kBlockThreads), 0, s, G.ids.p, G.data.p, P.perm.p, G.n, G.sdata.p,
+                       dim3(cse::kBlockThreads), 0, s, G.ids.p, G.data.p, P.perm.p, P.nperm, G.sdata.p,
                        G.sid1.p);
     CSE_HIP(hipGetLastError());
     G.sorted_ready = true;
@@ -891,6 +1019,11 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
   cg.loss.scale = G.loss.scale;
   cg.loss.scaled = G.loss.scaled;
   cg.apply_loss = ev->opts.apply_loss_function;
+  if (G.const0) {  // active cameras' state offsets need not be affine
+    cg.packed0 = G.packed0.p;
+    cg.packed_lo = G.slot0_lo;
+    cg.packed_stride = G.packed_stride;
+  }
   const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
   if (P.nchunks > 0) {
     auto launch = [&](auto kd) {
@@ -917,6 +1050,7 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
   ga.lo = P.lo;
   ga.grad = out;
   ga.delta_base = G.delta_base[0];
+  ga.delta_tab = G.const0 ? G.delta0.p + (P.lo - G.slot0_lo) : nullptr;
   const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
   hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
                      dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
@@ -1022,7 +1156,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     Group& G = ev->groups[g];
     if (G.n == 0) continue;
     const bool dma = G.packed0.p != nullptr;
-    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma);
+    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma, G.const0);
     if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
     // Gradient: a deterministic post-pass over the written residuals and
     // Jacobian when the group has plans for all its slots, else in-kernel
@@ -1030,8 +1164,13 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     bool grad_pass = d_grad && d_res && d_jac && G.affine && ev->opts.gradient_mode != 2;
     for (int j = 0; j < G.shape.nb; ++j) grad_pass = grad_pass && G.grad[j].ready;
     const int mode = ev->opts.gradient_mode;
-    const bool fused = grad_pass && G.fuse_ok && (mode == 0 || mode == 3);
-    const bool recompute = fused && mode == 0;  // slot 0 by CameraGradientKernel
+    // Mode 1 (post-pass) has no form over the packed F cells of a group with
+    // constant slot-0 blocks: it takes mode 0's fused form (also fixed order).
+    const bool fused = grad_pass && G.fuse_ok && (mode == 0 || mode == 3 || (mode == 1 && G.const0));
+    // Constant slot-0 blocks: no post-pass over the packed F cells (in-kernel
+    // atomics instead, active cameras only).
+    if (G.const0 && !fused) grad_pass = false;
+    const bool recompute = fused && mode != 3;  // slot 0 by CameraGradientKernel
     cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
     if (fused) {
       const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
@@ -1041,7 +1180,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       a.gfused = d_grad;
       a.gside = G.gside.p;
       a.gcontrib = G.gcontrib.p;
-      fn = PickFused(G.kind, G.loss.kind, G.policy, recompute);
+      fn = PickFused(G.kind, G.loss.kind, G.policy, recompute, G.const0);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma) {
@@ -1049,7 +1188,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       const int64_t total = G.slot0_count * pieces;
       hipLaunchKernelGGL(cse::RepackSlot0Kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                          ev->stream, d_state, G.state_base[0], G.shape.x0, G.packed_stride, pieces,
-                         G.slot0_lo, G.slot0_count, G.packed0.p);
+                         G.slot0_lo, G.slot0_count, G.packed0.p, G.src0.p, ev->cstate.p);
     }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
@@ -1256,6 +1395,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     ev->bytes_jac += per_block * g.num_blocks;
     G.policy = ev->opts.force_general_layout ? kTable : DetectAffine(d, g, k, &G);
     G.affine = G.policy != kTable;
+    if (!G.affine) G.const0 = false;  // DetectAffine may have set it before giving up
     if (G.affine && g.functor_kind == CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 &&
         d->parameter_blocks[g.parameter_block_ids[0]].manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
       // Slot 0 on the quaternion manifold (DetectAffine checked every
@@ -1263,6 +1403,20 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       G.kind = kKindQuaternionTangent;
       ShapeOf(G.kind, &G.shape);
     }
+    // Constant slot-0 blocks need the repacked table (their values come from
+    // the constant state through it).
+    if (G.const0 && G.slot0_count > (1 << 20)) {
+      G.policy = kTable;
+      G.affine = false;
+      G.const0 = false;
+      if (G.kind == kKindQuaternionTangent) {
+        G.kind = g.functor_kind;
+        ShapeOf(G.kind, &G.shape);
+      }
+    }
+    // Table-path tables: also for const0 groups (their J products use the
+    // table kernels).
+    if (G.const0) ev->any_general = true;
     if (!G.affine) ev->any_general = true;
     if (G.affine) {
       const int64_t chunks = (g.num_blocks + cse::kWave - 1) / cse::kWave;
@@ -1279,15 +1433,50 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     if (G.affine && G.slot0_count > 0 && G.slot0_count <= (1 << 20) &&
         (rc = G.packed0.alloc((size_t)G.slot0_count * G.packed_stride)))
       return bail(rc);
+    if (G.const0) {
+      std::vector<uint32_t> bits((size_t)((G.slot0_count + 31) / 32), 0u);
+      std::vector<int64_t> src((size_t)G.slot0_count, 0), dlt((size_t)G.slot0_count, -1);
+      // Ids in the range that are not camera-sized rows in bounds (blocks no
+      // block of the group uses) repack the first active camera (never read).
+      const int64_t fallback = G.state_base[0] + (int64_t)k.x0 * G.slot0_lo;  // overwritten below
+      int64_t first_active = -1;
+      for (int64_t q = 0; q < G.slot0_count && first_active < 0; ++q) {
+        const cse_parameter_block& pb = d->parameter_blocks[G.slot0_lo + q];
+        if (!pb.is_constant && pb.size == k.x0) first_active = pb.state_offset;
+      }
+      for (int64_t q = 0; q < G.slot0_count; ++q) {
+        const cse_parameter_block& pb = d->parameter_blocks[G.slot0_lo + q];
+        const bool fits = pb.size == k.x0 && pb.state_offset >= 0 &&
+                          pb.state_offset + k.x0 <= (pb.is_constant ? d->num_constant_parameters
+                                                                    : d->num_parameters);
+        if (!fits) {
+          src[q] = first_active >= 0 ? first_active : fallback;
+        } else if (pb.is_constant) {
+          src[q] = -1 - pb.state_offset;
+        } else {
+          bits[q >> 5] |= 1u << (q & 31);
+          src[q] = pb.state_offset;
+          dlt[q] = pb.delta_offset;
+        }
+      }
+      if ((rc = G.act0.upload(bits.data(), bits.size(), s))) return bail(rc);
+      if ((rc = G.src0.upload(src.data(), src.size(), s))) return bail(rc);
+      if ((rc = G.delta0.upload(dlt.data(), dlt.size(), s))) return bail(rc);
+      if (!G.h_fbase.empty() && (rc = G.fbase.upload(G.h_fbase.data(), G.h_fbase.size(), s)))
+        return bail(rc);
+      if (hipStreamSynchronize(s) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "upload failed"));
+    }
     if (G.affine && ev->has_layout) {
       const int sizes[2] = {k.s0, k.s1};
       for (int j = 0; j < k.nb; ++j)
-        if (GradSupported(k.nr, sizes[j]) && (rc = BuildGradPlan(g, k, j, &G.grad[j], s)))
+        if (GradSupported(k.nr, sizes[j]) &&
+            (rc = BuildGradPlan(g, k, j, &G.grad[j], s,
+                                j == 0 && G.const0 ? d->parameter_blocks : nullptr)))
           return bail(rc);
     }
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
     if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
-    if (!G.affine && g.residual_block_index &&
+    if ((!G.affine || G.const0) && g.residual_block_index &&
         (rc = G.gindex.upload(g.residual_block_index, (size_t)g.num_blocks, s)))
       return bail(rc);
     ev->groups.push_back(std::move(G));
@@ -1456,7 +1645,10 @@ int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double
   CSE_HIP(hipSetDevice(ev->device));
   for (auto& G : ev->groups) {
     if (G.n == 0) continue;
-    bool plans = G.affine;
+    // Groups with constant slot-0 blocks take the table kernels (their F
+    // cells are not at affine offsets).
+    const bool affine = G.affine && !G.const0;
+    bool plans = affine;
     for (int j = 0; j < G.shape.nb; ++j) plans = plans && G.grad[j].ready;
     // MakeArgs wants non-const outputs; the kernels only read a.jacobian.
     cse::GroupArgs a = MakeArgs(ev, G, nullptr, nullptr, const_cast<double*>(J), nullptr);
@@ -1482,7 +1674,7 @@ int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double
     } else {
       if (!G.affine && !ev->any_general)
         return Fail(CSE_ERR_UNSUPPORTED, "table-path tables were not uploaded");
-      if (!DispatchMultiply(G.kind, a, G.affine, left, x, y, ev->stream))
+      if (!DispatchMultiply(G.kind, a, affine, left, x, y, ev->stream))
         return Fail(CSE_ERR_UNSUPPORTED, "no multiply kernel for functor kind " +
                                              std::to_string(G.kind));
     }
@@ -1517,7 +1709,7 @@ int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const 
                        dim3((unsigned)((ev->num_effective + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                        dim3(cse::kBlockThreads), 0, s, d_D, d_x, d_y, ev->num_effective);
   bool fused = true;
-  for (auto& G : ev->groups) fused = fused && (G.n == 0 || G.fuse_ok);
+  for (auto& G : ev->groups) fused = fused && (G.n == 0 || (G.fuse_ok && !G.const0));
   if (!fused) {
     // z = J x, then y += J^T z: the two products of CudaCgnrLinearOperator.
     int rc;
@@ -1852,7 +2044,10 @@ int cse_get_info(cse_evaluator* ev, cse_info* info) {
   for (auto& G : ev->groups) {
     info->num_affine_groups += G.affine ? 1 : 0;
     info->num_fused_gradient_groups +=
-        (G.fuse_ok && (ev->opts.gradient_mode == 0 || ev->opts.gradient_mode == 3)) ? 1 : 0;
+        (G.fuse_ok && (ev->opts.gradient_mode == 0 || ev->opts.gradient_mode == 3 ||
+                       (ev->opts.gradient_mode == 1 && G.const0)))
+            ? 1
+            : 0;
   }
   info->device = ev->device;
   info->bytes_jacobian_eval = ev->bytes_jac;

@@ -36,10 +36,14 @@ namespace cse {
 //       columns, at [row0 + kR*N*i0, + kR*N*nw)
 //   kHalves (CRS): the rows staged and written for lanes [0, 32), then for
 //       lanes [32, 64), through half the LDS.
-template <class K, bool kJac, bool kCrs, bool kHalves = false>
+//   kConst0 (BlockSparseMatrix): lanes with a constant slot-0 block (act0
+//       false) have no F cell; the others' cells are packed in lane order from
+//       fbase[c] (chunk c).
+template <class K, bool kJac, bool kCrs, bool kHalves = false, bool kConst0 = false>
 __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
                                               int64_t i0, int nw, const double* r,
-                                              const double* J0, const double* J1) {
+                                              const double* J0, const double* J1,
+                                              bool act0 = true, int64_t c = 0) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   constexpr int N = S0 + S1;
@@ -82,12 +86,24 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
     } else {
       // Two rounds through the same LDS (slot 0's cells, then slot 1's): the
       // fast tail may size the staging buffer for slot 0 alone.
-      if (active) {
+      if constexpr (kConst0) {
+        const uint64_t m = __ballot(active && act0);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (active && act0) {
 #pragma unroll
-        for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
+          for (int q = 0; q < NR * S0; ++q) st[rank * NR * S0 + q] = J0[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        WaveStore(st, a.jacobian + a.fbase[c], __popcll(m) * NR * S0, lane);
+      } else {
+        if (active) {
+#pragma unroll
+          for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
       }
-      __builtin_amdgcn_wave_barrier();
-      WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
       if constexpr (S1 > 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
@@ -371,8 +387,8 @@ struct FusedGrad {
 
 // Can the wave take the back-to-back store tail?  Full chunk, 16-byte
 // pieces that tile every segment exactly, 16-byte-aligned destinations.
-template <class K, bool kJac, bool kCrs>
-__device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw) {
+template <class K, bool kJac, bool kCrs, bool kConst0 = false>
+__device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw, int64_t c = 0) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, N = S0 + S1;
   if (nw != kWave) return false;
@@ -392,7 +408,8 @@ __device__ __forceinline__ bool FastTail(const GroupArgs& a, int64_t i0, int nw)
                                                                          : a.jac_base[Tr::NB - 1][0];
       m |= reinterpret_cast<uintptr_t>(a.jacobian + row0 + (int64_t)NR * N * i0);
     } else {
-      m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0);
+      m |= reinterpret_cast<uintptr_t>(
+          a.jacobian + (kConst0 ? a.fbase[c] : a.jac_base[0][0] + a.jac_stride[0] * i0));
       if constexpr (S1 > 0)
         m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0);
     }
@@ -490,7 +507,7 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
           int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
-          int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0>
+          int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0, bool kConst0_ = false>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -507,6 +524,7 @@ struct Tune {
   static constexpr int kEPol = kEPol_;  // StoreNt16 policy of the E-cell stores
   static constexpr int kRPol = kRPol_;  // and of the residual stores
   static constexpr int kFPol = kFPol_;  // and of the F-cell stores
+  static constexpr bool kConst0 = kConst0_;  // constant slot-0 blocks (BSM)
 };
 // Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
 // sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
@@ -517,6 +535,11 @@ struct Tune {
 using ShippedTune = Tune<0, true, true>;
 // The fused gradient's points-only form (CameraGradientKernel adds slot 0).
 using PointsOnlyTune = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true>;
+// The same for groups with constant slot-0 blocks (a held camera): a wave
+// with one takes the slow tail, its F cells packed from fbase[c]; waves
+// without take the fast tail from fbase[c].
+using ShippedTuneC0 = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 0, 0, true>;
+using PointsOnlyTuneC0 = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true, 0, 0, 0, true>;
 
 // Does the shipped BSM Jacobian kernel of kind K stage in two rounds (and so
 // fit 4 workgroups per CU)?
@@ -625,8 +648,17 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   }
   const double cost =
       LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
+  bool act0 = true;  // slot-0 block active (T::kConst0: from its bit)
+  if constexpr (T::kConst0) {
+    static_assert(!kCrs && kCoop == 2, "constant slot-0 blocks: BlockSparseMatrix, repacked table");
+    const uint32_t k0 = (uint32_t)(in.id0 - a.packed0_lo);
+    act0 = ((a.act0_bits[k0 >> 5] >> (k0 & 31)) & 1u) != 0;
+  }
   if (kJac && a.gradient != nullptr && active) {
-    AddGradientSlot<NR, S0>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0, S0, r, J0);
+    if (act0)
+      AddGradientSlot<NR, S0>(a.gradient + (T::kConst0 ? a.delta0[in.id0 - a.packed0_lo]
+                                                        : a.delta_base[0] + (int64_t)S0 * in.id0),
+                              S0, r, J0);
     if constexpr (S1 > 0)
       AddGradientSlot<NR, S1p>(a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1, S1, r, J1);
   }
@@ -639,8 +671,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   FusedGrad<K> fg;
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
-  if (!FastTail<K, kJac, kCrs>(a, i0, nw)) {
-    StageAndStore<K, kJac, kCrs, kTwoCrs>(a, st, lane, active, i0, nw, r, J0, J1);
+  bool fast = FastTail<K, kJac, kCrs, T::kConst0>(a, i0, nw, c);
+  if constexpr (T::kConst0) fast = fast && __ballot(!act0) == 0;
+  if (!fast) {
+    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;
@@ -733,7 +767,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
           }
           seg1 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0;
         }
-        seg0 = a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0;
+        seg0 = a.jacobian + (T::kConst0 ? a.fbase[c] : a.jac_base[0][0] + a.jac_stride[0] * i0);
       }
       if constexpr (!kTwoCrs) {
         __builtin_amdgcn_wave_barrier();
@@ -905,10 +939,10 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const Grou
 
 // The shipped BSM Jacobian kernel of two-slot kinds: two-round staging (36
 // KiB of LDS a workgroup, 4 per CU) held to 4 waves per SIMD (128 VGPRs).
-template <class K, int kLoss, int kCoop>
+template <class K, int kLoss, int kCoop, class T = ShippedTune>
 __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound(const GroupArgs a) {
   static_assert(kTwoRoundBsm<K>, "two-slot kinds");
-  AffineChunkBody<K, kLoss, true, false, kCoop, false, ShippedTune>(a);
+  AffineChunkBody<K, kLoss, true, false, kCoop, false, T>(a);
 }
 
 // The shipped CRS Jacobian kernel: rows staged in two half-waves (24 KiB of
@@ -930,10 +964,10 @@ __global__ __launch_bounds__(kBlockThreads, kMinWaves) void EvaluateAffineChunks
 // The fused-gradient form of the hot kernel, held to 3 waves per SIMD
 // (168 VGPRs): the LDS bound of 3 workgroups per CU.  Unbounded, the CRS
 // form takes 170 VGPRs and drops to 2.
-template <class K, int kLoss, bool kCrs>
+template <class K, int kLoss, bool kCrs, class T = ShippedTune>
 __global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(3))) void
 EvaluateAffineChunksFused(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, true, kCrs, 2, true>(a);
+  AffineChunkBody<K, kLoss, true, kCrs, 2, true, T>(a);
 }
 
 // The fused gradient's points-only form: the slot-1 rows and boundary
@@ -941,10 +975,10 @@ EvaluateAffineChunksFused(const GroupArgs a) {
 // the slot-0 sums).  Without the contribution registers both forms fit 128
 // VGPRs and run at 4 waves per SIMD (CRS with the half-wave staging: 2.33 ->
 // 2.25 ms against 3 waves, profiles/round2/s5l).
-template <class K, int kLoss, bool kCrs>
+template <class K, int kLoss, bool kCrs, class T = PointsOnlyTune>
 __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksFusedPoints(
     const GroupArgs a) {
-  AffineChunkBody<K, kLoss, true, kCrs, 2, true, PointsOnlyTune>(a);
+  AffineChunkBody<K, kLoss, true, kCrs, 2, true, T>(a);
 }
 
 // Slot-0 (camera) part of the fused gradient, by re-evaluation in camera
@@ -977,6 +1011,11 @@ struct CamGradArgs {
   int64_t nchunks;
   LossParams loss;
   int apply_loss;
+  // Groups with constant slot-0 blocks: the camera from the repacked table
+  // (row id - packed_lo), whose state offsets need not be affine.
+  const double* packed0;
+  int32_t packed_lo;
+  int32_t packed_stride;
 };
 
 // r and the slot-0 Jacobian (NR x S0, row-major) of one block, the slot-1
@@ -1016,7 +1055,8 @@ __global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamG
   if (cid >= g.nchunks) return;
   const int64_t q0 = g.chunk_begin[cid], q1 = g.chunk_begin[cid + 1];
   constexpr int X0 = Tr::X0;
-  const double* cam = g.state + g.state_base0 + (int64_t)X0 * g.chunk_pb[cid];
+  const double* cam = g.packed0 ? g.packed0 + (int64_t)g.packed_stride * (g.chunk_pb[cid] - g.packed_lo)
+                                : g.state + g.state_base0 + (int64_t)X0 * g.chunk_pb[cid];
   double x0[X0];
 #pragma unroll
   for (int k = 0; k < X0; ++k) x0[k] = cam[k];

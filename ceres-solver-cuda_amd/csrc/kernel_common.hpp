@@ -56,6 +56,12 @@ struct GroupArgs {
   const double* packed0;
   int32_t packed0_lo;
   int32_t packed0_stride;  // doubles per row: PackedRowDoubles(S0)
+  // Constant slot-0 blocks (a held camera, BlockSparseMatrix only): bit
+  // (id - packed0_lo) of act0_bits set = active; the F cells of the active
+  // blocks of chunk c start at fbase[c] (no cell for a constant block).
+  const uint32_t* act0_bits;
+  const int64_t* fbase;
+  const int64_t* delta0;  // [slot-0 id - packed0_lo] delta offset of an active block
   // Table policy.
   const int64_t* gindex;
   int64_t first;

@@ -36,6 +36,7 @@ struct GradArgs {
   int32_t lo;
   double* grad;
   int64_t delta_base;   // delta offset of id = delta_base + S * id
+  const int64_t* delta_tab;  // GradientChunkReduceKernel: [count] offsets instead (may be null)
 };
 
 template <int NR, int S, bool kWaveMode>
@@ -138,13 +139,15 @@ __global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const
                                                                            const GradChunks ch) {
   const int64_t p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
   if (p >= g.count) return;
+  // A block without chunks adds nothing (and a constant one has no row).
+  if (ch.chunk_off[p] == ch.chunk_off[p + 1]) return;
   double acc[S];
 #pragma unroll
   for (int c = 0; c < S; ++c) acc[c] = 0.0;
   for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q)
 #pragma unroll
     for (int c = 0; c < S; ++c) acc[c] += ch.partial[q * S + c];
-  double* dst = g.grad + g.delta_base + (int64_t)S * (g.lo + p);
+  double* dst = g.grad + (g.delta_tab ? g.delta_tab[p] : g.delta_base + (int64_t)S * (g.lo + p));
 #pragma unroll
   for (int c = 0; c < S; ++c) dst[c] += acc[c];
 }
@@ -590,14 +593,23 @@ __global__ __launch_bounds__(kBlockThreads) void ReduceFinalizeKernel(
 // packed table (once per evaluation: 13,682 cameras = 1.1 MB for BAL
 // problem-13682), one 16-byte piece per thread: the first `pieces` pieces of
 // each row of `stride` doubles (the LDS-DMA gather reads no others).
+// With src_off (groups with constant slot-0 blocks): row b comes from
+// state + src_off[b] (active) or cstate + (-1 - src_off[b]) (constant).
 __global__ __launch_bounds__(256) void RepackSlot0Kernel(const double* state, int64_t state_base,
                                                          int size, int stride, int pieces, int32_t lo,
-                                                         int64_t count, double* packed) {
+                                                         int64_t count, double* packed,
+                                                         const int64_t* src_off, const double* cstate) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t b = t / pieces;
   const int k = 2 * (int)(t - b * pieces);
   if (b >= count) return;
-  const double* src = state + state_base + (int64_t)size * (lo + b);
+  const double* src;
+  if (src_off) {
+    const int64_t o = src_off[b];
+    src = o >= 0 ? state + o : cstate + (-1 - o);
+  } else {
+    src = state + state_base + (int64_t)size * (lo + b);
+  }
   const double x = src[k];
   const double y = k + 1 < size ? src[k + 1] : 0.0;
   *reinterpret_cast<double2*>(packed + (int64_t)stride * b + k) = make_double2(x, y);

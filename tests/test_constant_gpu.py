@@ -1,0 +1,172 @@
+"""GPU: held (constant) cameras on the affine kernels.
+
+Problem::SetParameterBlockConstant on a camera -- e.g. to fix the gauge of a
+bundle adjustment -- removes its columns: in the BlockSparseMatrix the blocks
+of that camera have no F cell, so every later block's F cell moves up by one
+cell (block_jacobian_writer.cc:75-149), and the camera's values come from the
+constant state (registered_cuda_evaluators.cc:237-248).  Groups whose slot-0
+blocks are partly constant stay on the affine kernels
+(cse::ShippedTuneC0: F cells packed in block order from a per-chunk base, waves
+with a held camera through the slow tail); CompressedRowSparseMatrix falls
+back to the table path.  Against the oracle (tests/parity_util.py
+tolerances): both layouts, losses, the four gradient modes, residual/cost-only,
+ragged sizes, whole chunks of held cameras, the quaternion manifold, the
+Jacobian products and the multi-device evaluator; the reference's own mix is
+the mini-BA of evaluator_cuda_test.cu.cc:232-459 (test_parity_gpu.py).
+"""
+import numpy as np
+import pytest
+
+import ceres_amd as ca
+from ceres_amd import bal
+import oracle_py as O
+from parity_util import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_eval(prog, threads=8, **kw):
+    ex = prog.with_explicit_manifolds()
+    op = O.OracleProgram.from_program(ex)
+    return op.evaluate(ex.state, ex.constant_state if ex.constant_state.size else None,
+                       num_threads=threads, **kw)
+
+
+def gpu_eval(prog, **opts):
+    ev = ca.Evaluator(prog, **opts)
+    try:
+        return ev.evaluate(), ev.info()
+    finally:
+        ev.close()
+
+
+def held(counts=(16, 700, 2900), const=(0,), loss=None, fmt=ca.BLOCK_SPARSE, seed=13, **kw):
+    return bal.synthetic_program(counts, loss=loss, format=fmt, seed=seed, constant_cameras=const,
+                                 **kw)
+
+
+@pytest.mark.parametrize("const", [(0,), (7,), (15,), (0, 3, 9, 15)])
+@pytest.mark.parametrize("loss", [None, ca.Loss.huber(1.0), ca.Loss.cauchy(2.0)])
+def test_held_cameras_bsm_affine(gpu, const, loss):
+    prog = held(const=const, loss=loss)
+    assert prog.num_effective_parameters == 3 * 700 + 9 * (16 - len(const))
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog)
+    assert info.num_affine_groups == 1
+    assert_parity(got, ref, (const, loss))
+    tab, info = gpu_eval(prog, force_general_layout=True)
+    assert info.num_affine_groups == 0
+    assert_parity(tab, ref, (const, loss, "table"))
+    assert np.array_equal(got[2], tab[2]) and np.array_equal(got[4], tab[4])
+
+
+def test_held_cameras_crs_takes_the_table_path(gpu):
+    prog = held(const=(2, 5), loss=ca.Loss.huber(1.0), fmt=ca.COMPRESSED_ROW)
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog)
+    assert info.num_affine_groups == 0
+    assert_parity(got, ref, "crs")
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_held_cameras_every_gradient_mode(gpu, mode):
+    prog = held(const=(0, 11), loss=ca.Loss.huber(1.0), seed=3)
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog, gradient_mode=mode)
+    assert info.num_affine_groups == 1
+    # mode 1 has no post-pass over packed F cells: the fused form (mode 0) runs
+    assert info.num_fused_gradient_groups == (0 if mode == 2 else 1)
+    assert_parity(got, ref, ("gradient_mode", mode))
+    if mode != 2:  # fixed-order sums: bit-identical repeats
+        again, _ = gpu_eval(prog, gradient_mode=mode)
+        assert all(np.array_equal(x, y) for x, y in zip(got[2:], again[2:]))
+
+
+@pytest.mark.parametrize("n_obs", [1, 63, 64, 65, 130, 1000])
+def test_held_cameras_ragged(gpu, n_obs):
+    prog = held(counts=(4, max(1, n_obs // 3), n_obs), const=(1,), seed=n_obs)
+    ref = oracle_eval(prog)
+    got, _ = gpu_eval(prog)
+    assert_parity(got, ref, n_obs)
+
+
+def test_chunks_whose_cameras_are_all_held(gpu):
+    # Most cameras held: whole 64-block chunks without an F cell.
+    prog = held(counts=(10, 2000, 9000), const=tuple(range(1, 10)), loss=ca.Loss.huber(1.0))
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog)
+    assert info.num_affine_groups == 1
+    assert_parity(got, ref, "mostly held")
+
+
+def test_held_cameras_residual_and_cost_only(gpu):
+    prog = held(const=(4,), loss=ca.Loss.huber(1.0), seed=6)
+    ref = oracle_eval(prog, residuals=True, gradient=False, jacobian=False)
+    ev = ca.Evaluator(prog)
+    got = ev.evaluate(residuals=True, gradient=False, jacobian=False)
+    cost = ev.evaluate(residuals=False, gradient=False, jacobian=False)
+    ev.close()
+    assert_parity(got, ref, "residuals")
+    assert cost[1] == got[1]
+
+
+def test_held_quaternion_camera_on_its_manifold(gpu):
+    prog = held(const=(0, 8), loss=ca.Loss.cauchy(1.0), quaternion_manifold=True, seed=9)
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog)
+    assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
+    assert_parity(got, ref, "quaternion held")
+
+
+def test_held_cameras_jacobian_products(gpu):
+    torch = pytest.importorskip("torch")
+    from test_spmv_gpu import dense_jacobian
+    prog = held(const=(0, 6), loss=ca.Loss.huber(1.0), seed=12)
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
+    ok, cost, r, g, jv = ev.evaluate()
+    assert ok
+    J = dense_jacobian(prog, jv)
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=prog.num_effective_parameters)
+    z = rng.normal(size=prog.num_residuals)
+    D = rng.uniform(0.5, 1.5, prog.num_effective_parameters)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dj, dx, dz, dD = t(jv), t(x), t(z), t(D)
+    jx = torch.zeros(prog.num_residuals, dtype=torch.float64, device=dev)
+    jtz = torch.zeros(prog.num_effective_parameters, dtype=torch.float64, device=dev)
+    cg = torch.zeros(prog.num_effective_parameters, dtype=torch.float64, device=dev)
+    ev.right_multiply_device(dj.data_ptr(), dx.data_ptr(), jx.data_ptr())
+    ev.left_multiply_device(dj.data_ptr(), dz.data_ptr(), jtz.data_ptr())
+    ev.cgnr_multiply_device(dj.data_ptr(), dD.data_ptr(), dx.data_ptr(), cg.data_ptr())
+    torch.cuda.synchronize(dev)
+    ev.close()
+    close = lambda a, b: np.linalg.norm(a - b) <= 1e-12 * np.linalg.norm(b)
+    assert close(jx.cpu().numpy(), J @ x)
+    assert close(jtz.cpu().numpy(), J.T @ z)
+    assert close(cg.cpu().numpy(), J.T @ (J @ x) + D * D * x)
+
+
+def test_held_cameras_multi_device(gpu):
+    prog = held(counts=(20, 3001, 21113), const=(0, 13), loss=ca.Loss.huber(1.0), seed=4)
+    ref = oracle_eval(prog)
+    ev = ca.Evaluator(prog, devices=[0, 0, 0])
+    got = ev.evaluate()
+    info = ev.info()
+    ev.close()
+    assert info.num_affine_groups == 1
+    assert_parity(got, ref, "multi-device held")
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_problem_13682_one_held_camera(gpu):
+    """problem-13682 with its first camera held (the gauge), Huber, BSM."""
+    prog = bal.synthetic_program("problem-13682-4456117", loss=ca.Loss.huber(1.0),
+                                 constant_cameras=(0,))
+    got, info = gpu_eval(prog)
+    assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
+    ref = oracle_eval(prog, threads=16)
+    rep = {}
+    assert_parity(got, ref, "problem-13682 held camera", report=rep)
+    print("problem-13682 one-held-camera parity:", rep)

@@ -27,7 +27,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, fmt, q):
+def _worker(rank, world, port, fmt, q, held=()):
     import sys
     for p in (os.path.join(REPO, "ceres-solver-cuda_amd"), os.path.join(REPO, "oracle"),
               os.path.join(REPO, "tests")):
@@ -43,19 +43,22 @@ def _worker(rank, world, port, fmt, q):
         C, P, Obs = 12, 700, 2600
         cams, pts, ci, pi, obs = bal.synthetic(C, P, Obs, seed=21)
         loss = ca.Loss.huber(1.0)
-        prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss, format=fmt)
-        ok, cost, r, g, j = O.OracleProgram.from_program(prog).evaluate(prog.state, num_threads=2)
+        prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss, format=fmt,
+                                       constant_cameras=held)
+        cs = prog.constant_state if prog.constant_state.size else None
+        ok, cost, r, g, j = O.OracleProgram.from_program(prog).evaluate(prog.state, cs, num_threads=2)
         assert ok
         c = torch.tensor([cost], dtype=torch.float64)
         dist.all_reduce(c)
-        pmap, cmap = shard.gradient_maps(sh, P, C)
+        pmap, cmap = shard.gradient_maps(sh, P, C - len(held))
         gcam = torch.from_numpy(g[cmap[0]:cmap[0] + cmap[2]].copy())
         dist.all_reduce(gcam)
         parts = [None] * world
         dist.all_gather_object(parts, (sh, r, j, g[pmap[0]:pmap[0] + pmap[2]].copy()))
         if rank == 0:
-            full = bal.program(cams, pts, ci, pi, obs, loss=loss, format=fmt)
-            okf, costf, rf, gf, jf = O.OracleProgram.from_program(full).evaluate(full.state,
+            full = bal.program(cams, pts, ci, pi, obs, loss=loss, format=fmt, constant_cameras=held)
+            fcs = full.constant_state if full.constant_state.size else None
+            okf, costf, rf, gf, jf = O.OracleProgram.from_program(full).evaluate(full.state, fcs,
                                                                               num_threads=2)
             assert okf
             assert abs(float(c.item()) - costf) <= 1e-12 * abs(costf)
@@ -78,12 +81,14 @@ def _worker(rank, world, port, fmt, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("fmt", ["block_sparse", "compressed_row"])
-def test_sharded_evaluation_matches_unsharded(world, fmt):
+@pytest.mark.parametrize("fmt,held", [("block_sparse", ()), ("compressed_row", ()),
+                                      ("block_sparse", (0, 5))])
+def test_sharded_evaluation_matches_unsharded(world, fmt, held):
+    # held: cameras held constant (their blocks have no F cell; Shard.f_cells)
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, q, held)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
