@@ -203,16 +203,21 @@ def solve(args):
     max_radius = 1e16  # Solver::Options::max_trust_region_radius
     min_relative_decrease = 1e-3  # Solver::Options::min_relative_decrease
     rows = []
-    D = None
+    D = torch.zeros(n, dtype=f64, device=dev)
+    ones = torch.ones(m, dtype=f64, device=dev)
+    jac2 = None  # squared Jacobian values, one buffer for the whole solve
+    d_stale = True  # D follows J: recomputed after the initial and each accepted evaluation
     for it in range(args.num_iterations):
         # Jacobi scaling: diag(J^T J) = column sums of squared values, one
         # left-multiply of the squared Jacobian with a vector of ones.
-        jac2 = jac * jac
-        D = torch.zeros(n, dtype=f64, device=dev)
-        ones = torch.ones(m, dtype=f64, device=dev)
-        ev.left_multiply_device(jac2.data_ptr(), ones.data_ptr(), D.data_ptr())
-        D.clamp_(min=1e-6)
-        del jac2
+        if d_stale:
+            if jac2 is None:
+                jac2 = torch.empty_like(jac)
+            torch.mul(jac, jac, out=jac2)
+            D.zero_()
+            ev.left_multiply_device(jac2.data_ptr(), ones.data_ptr(), D.data_ptr())
+            D.clamp_(min=1e-6)
+            d_stale = False
         solver = schur_solve if args.linear_solver == "iterative_schur" else cgnr
         dx, cg_iters = timed("Linear solver", lambda: solver(1.0 / radius))
         timed("Plus", lambda: ev.plus_device(x.data_ptr(), dx.data_ptr(), cand.data_ptr()))
@@ -238,11 +243,13 @@ def solve(args):
             x.copy_(cand)
             if timed("Jacobian & residual evaluation", jacobian_eval) != 0:
                 raise SystemExit(f"iteration {it}: Jacobian evaluation at the accepted point failed")
+            d_stale = True
             radius = min(max_radius, radius / max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3))
             decrease_factor = 2.0
         else:
             radius = radius / decrease_factor
             decrease_factor *= 2.0
+    del jac2
     ev.close()
     print("iter      cost      cost_new   |gradient|    |step|    tr_radius  ls_iter  accepted")
     for it, c0, c1, gn, sn, rad, li, acc in rows:

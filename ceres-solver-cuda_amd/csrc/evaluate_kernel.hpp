@@ -139,6 +139,7 @@ template <class K>
 struct AffineInputs {
   double d[KindTraits<K>::D];
   double x0[KindTraits<K>::X0];  // ambient values
+  double x0pad;                   // the repacked row's padding double (odd X0): 1.0 = constant
   double x1[KindTraits<K>::S1p];
   int32_t id0, id1;
 };
@@ -249,6 +250,7 @@ __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int
   } else {
 #pragma unroll
     for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
+    if constexpr (X0 < X0p) in->x0pad = lds[lane * X0p + X0];
   }
   __builtin_amdgcn_wave_barrier();
   in->id0 = id.x;
@@ -651,8 +653,12 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   bool act0 = true;  // slot-0 block active (T::kConst0: from its bit)
   if constexpr (T::kConst0) {
     static_assert(!kCrs && kCoop == 2, "constant slot-0 blocks: BlockSparseMatrix, repacked table");
-    const uint32_t k0 = (uint32_t)(in.id0 - a.packed0_lo);
-    act0 = ((a.act0_bits[k0 >> 5] >> (k0 & 31)) & 1u) != 0;
+    if constexpr ((Tr::X0 & 1) != 0 && !T::kDmaOwn) {
+      act0 = in.x0pad == 0.0;  // the flag came with the row (RepackSlot0Kernel)
+    } else {
+      const uint32_t k0 = (uint32_t)(in.id0 - a.packed0_lo);
+      act0 = ((a.act0_bits[k0 >> 5] >> (k0 & 31)) & 1u) != 0;
+    }
   }
   if (kJac && a.gradient != nullptr && active) {
     if (act0)

@@ -611,7 +611,9 @@ __global__ __launch_bounds__(256) void RepackSlot0Kernel(const double* state, in
     src = state + state_base + (int64_t)size * (lo + b);
   }
   const double x = src[k];
-  const double y = k + 1 < size ? src[k + 1] : 0.0;
+  // The padding double of an odd-sized row marks a constant block (1.0):
+  // the constant-aware kernels read it with the row (AffineInputs::x0pad).
+  const double y = k + 1 < size ? src[k + 1] : (src_off && src_off[b] < 0 ? 1.0 : 0.0);
   *reinterpret_cast<double2*>(packed + (int64_t)stride * b + k) = make_double2(x, y);
 }
 

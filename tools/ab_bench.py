@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--lib", default=None, help="tuning library to load (default lib/libcse_tuning.so)")
     ap.add_argument("--mode", default="jacobian", choices=["jacobian", "gradient", "residual", "cost"])
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
+    ap.add_argument("--held-cameras", type=int, default=0,
+                    help="hold the first K cameras constant (the const0 kernels)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="time rank 0's shard of an N-way point-bucket cut instead")
     args = ap.parse_args()
@@ -57,7 +59,8 @@ def main():
         prog = shard.shard_program(*bal.synthetic(*bal.CONFIGS[args.config]), 0, args.shard_of,
                                    loss=loss, format=args.format)[0]
     else:
-        prog = bal.synthetic_program(args.config, loss=loss, format=args.format)
+        prog = bal.synthetic_program(args.config, loss=loss, format=args.format,
+                                     constant_cameras=tuple(range(args.held_cameras)))
     print(f"# built {args.config} in {time.time() - t0:.1f} s", flush=True)
     dev = torch.device("cuda", 0)
     f64 = torch.float64
