@@ -40,6 +40,11 @@ def parse(argv=None):
     src.add_argument("--input", help="BAL problem file (text)")
     src.add_argument("--synthetic", choices=list(bal.CONFIGS), help="synthetic BAL shape")
     ap.add_argument("--robustify", action="store_true", help="HuberLoss(1.0)")
+    ap.add_argument("--use_quaternions", action="store_true",
+                    help="10-parameter cameras {q, t, f, k1, k2} (bal_problem.cc:110-121)")
+    ap.add_argument("--use_manifolds", action="store_true",
+                    help="with --use_quaternions: every camera on ProductManifold<QuaternionManifold, "
+                         "EuclideanManifold<6>> (bundle_adjuster.cc:337-345)")
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
     ap.add_argument("--rotation_sigma", type=float, default=0.0)
     ap.add_argument("--translation_sigma", type=float, default=0.0)
@@ -90,7 +95,13 @@ def solve(args):
     bal.perturb(cams, pts, args.rotation_sigma, args.translation_sigma, args.point_sigma)
     order = bal.schur_residual_order(pi, pts.shape[0])
     loss = ca.Loss.huber(1.0) if args.robustify else None
-    prog = bal.program(cams, pts, ci[order], pi[order], obs[order], loss=loss, format=args.format)
+    if args.use_quaternions:
+        cams = bal.to_quaternion_cameras(cams)
+    manifold = args.use_quaternions and args.use_manifolds
+    if args.use_quaternions and not manifold and args.linear_solver == "iterative_schur":
+        raise SystemExit("iterative_schur takes 9-column cameras: add --use_manifolds or use cgnr")
+    prog = bal.program(cams, pts, ci[order], pi[order], obs[order], loss=loss, format=args.format,
+                       quaternion_manifold=manifold)
     timers.add("Preprocessor", time.perf_counter() - t0)
 
     stream = torch.cuda.current_stream(dev).cuda_stream

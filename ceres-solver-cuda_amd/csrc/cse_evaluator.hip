@@ -557,6 +557,9 @@ struct cse_evaluator {
   bool plus_supported = true;
   std::vector<cse::PlusRun> plus_runs_host;
   DevBuf<cse::PlusRun> plus_runs;
+  // CSE_MANIFOLD_QUATERNION_EUCLIDEAN blocks: Plus one block per thread.
+  std::vector<cse::QuatPlusBlock> plus_quat_host;
+  DevBuf<cse::QuatPlusBlock> plus_quat;
   DevBuf<double> h_delta, h_plus;
   DevBuf<int> status;  // [0] running flag, [1] last status, [2] reduce counter
   // Host-path buffers (allocated on first use).
@@ -1308,6 +1311,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
       const cse_parameter_block& pb = d->parameter_blocks[b];
       if (pb.is_constant) continue;
+      if (pb.manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
+        ev->plus_quat_host.push_back({pb.state_offset, pb.delta_offset, pb.size, 0});
+        continue;
+      }
       if (pb.plus_jacobian_offset >= 0 || pb.tangent_size != pb.size) ev->plus_supported = false;
       blocks.emplace_back(pb.state_offset, b);
     }
@@ -1938,19 +1945,33 @@ int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_de
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
   CSE_SINGLE_DEVICE(ev, "cse_plus_device");
   if (!ev->plus_supported)
-    return Fail(CSE_ERR_UNSUPPORTED, "Plus on device: an active parameter block has a manifold");
-  if (ev->plus_runs_host.empty()) return CSE_OK;
+    return Fail(CSE_ERR_UNSUPPORTED,
+                "Plus on device: an active parameter block has an explicit plus-Jacobian manifold");
+  if (ev->plus_runs_host.empty() && ev->plus_quat_host.empty()) return CSE_OK;
   if (!d_state || !d_delta || !d_state_plus_delta) return Fail(CSE_ERR_INVALID, "null pointer");
   CSE_HIP(hipSetDevice(ev->device));
-  if (!ev->plus_runs.p) {
-    int rc = ev->plus_runs.upload(ev->plus_runs_host.data(), ev->plus_runs_host.size(), ev->stream);
-    if (rc) return rc;
+  if (!ev->plus_runs_host.empty()) {
+    if (!ev->plus_runs.p) {
+      int rc = ev->plus_runs.upload(ev->plus_runs_host.data(), ev->plus_runs_host.size(), ev->stream);
+      if (rc) return rc;
+    }
+    const int64_t n = ev->num_parameters;
+    const unsigned grid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((n + cse::kBlockThreads - 1) / cse::kBlockThreads, 8LL * ev->num_cus));
+    hipLaunchKernelGGL(cse::PlusKernel, dim3(grid), dim3(cse::kBlockThreads), 0, ev->stream, d_state,
+                       d_delta, d_state_plus_delta, ev->plus_runs.p, (int)ev->plus_runs_host.size());
   }
-  const int64_t n = ev->num_parameters;
-  const unsigned grid = (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>((n + cse::kBlockThreads - 1) / cse::kBlockThreads, 8LL * ev->num_cus));
-  hipLaunchKernelGGL(cse::PlusKernel, dim3(grid), dim3(cse::kBlockThreads), 0, ev->stream, d_state,
-                     d_delta, d_state_plus_delta, ev->plus_runs.p, (int)ev->plus_runs_host.size());
+  if (!ev->plus_quat_host.empty()) {
+    if (!ev->plus_quat.p) {
+      int rc = ev->plus_quat.upload(ev->plus_quat_host.data(), ev->plus_quat_host.size(), ev->stream);
+      if (rc) return rc;
+    }
+    const int64_t nq = (int64_t)ev->plus_quat_host.size();
+    hipLaunchKernelGGL(cse::QuaternionPlusKernel,
+                       dim3((unsigned)((nq + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                       dim3(cse::kBlockThreads), 0, ev->stream, d_state, d_delta, d_state_plus_delta,
+                       ev->plus_quat.p, nq);
+  }
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }
@@ -1960,7 +1981,8 @@ int cse_plus(cse_evaluator* ev, const double* state, const double* delta,
   if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
   if (ev->multi) return MultiPlus(ev->multi, state, delta, state_plus_delta);
   if (!ev->plus_supported)
-    return Fail(CSE_ERR_UNSUPPORTED, "Plus on device: an active parameter block has a manifold");
+    return Fail(CSE_ERR_UNSUPPORTED,
+                "Plus on device: an active parameter block has an explicit plus-Jacobian manifold");
   if (ev->num_parameters == 0) return CSE_OK;
   if (!state || !delta || !state_plus_delta) return Fail(CSE_ERR_INVALID, "null pointer");
   CSE_HIP(hipSetDevice(ev->device));

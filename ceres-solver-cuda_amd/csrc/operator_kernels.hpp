@@ -509,6 +509,49 @@ __global__ __launch_bounds__(kBlockThreads) void PlusKernel(const double* x, con
   }
 }
 
+// Program::Plus of the CSE_MANIFOLD_QUATERNION_EUCLIDEAN blocks, one block
+// per thread: ProductManifold<QuaternionManifold, EuclideanManifold<n>>::Plus,
+// i.e. QuaternionPlusImpl (internal/ceres/manifold.cc:28-59: the quaternion
+// exp(delta) on the left of x, x unchanged when |delta| is zero) and x + delta
+// for the Euclidean tail.
+struct QuatPlusBlock {
+  int64_t state_offset;
+  int64_t delta_offset;
+  int32_t size;
+  int32_t pad;
+};
+
+__global__ __launch_bounds__(kBlockThreads) void QuaternionPlusKernel(const double* x,
+                                                                      const double* delta,
+                                                                      double* out,
+                                                                      const QuatPlusBlock* blocks,
+                                                                      int64_t n) {
+  const int64_t b = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (b >= n) return;
+  const QuatPlusBlock B = blocks[b];
+  const double* q = x + B.state_offset;
+  const double* d = delta + B.delta_offset;
+  double* o = out + B.state_offset;
+  const double n2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+  if (n2 == 0.0) {
+    o[0] = q[0];
+    o[1] = q[1];
+    o[2] = q[2];
+    o[3] = q[3];
+  } else {
+    const double nd = sqrt(n2);
+    double sn, cs;
+    sincos(nd, &sn, &cs);
+    const double sbd = sn / nd;
+    const double w = cs, a = sbd * d[0], bq = sbd * d[1], c = sbd * d[2];
+    o[0] = w * q[0] - a * q[1] - bq * q[2] - c * q[3];
+    o[1] = w * q[1] + a * q[0] + bq * q[3] - c * q[2];
+    o[2] = w * q[2] - a * q[3] + bq * q[0] + c * q[1];
+    o[3] = w * q[3] + a * q[2] - bq * q[1] + c * q[0];
+  }
+  for (int k = 4; k < B.size; ++k) o[k] = q[k] + d[k - 1];
+}
+
 // Sums the per-workgroup partials of every group in a fixed order, writes
 // the cost, publishes the evaluation status and re-arms the status word
 // for the next evaluation (replaces thrust::reduce + the abort-flag round

@@ -119,7 +119,8 @@ typedef struct cse_parameter_block {
  *       identity block) from the block's current value in registers; the
  *       result equals the dense product with that matrix.  Blocks of this kind
  *       in slot 0 of SNAVELY_QUATERNION_2_10_3 groups keep the affine (fast)
- *       kernels; Plus on device is not available for them. */
+ *       kernels; cse_plus applies QuaternionPlusImpl (manifold.cc:28-59) to
+ *       them and x + delta to the Euclidean part. */
 typedef enum cse_manifold_kind {
   CSE_MANIFOLD_MATRIX = 0,
   CSE_MANIFOLD_QUATERNION_EUCLIDEAN = 1
@@ -235,11 +236,12 @@ int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians);
 
 /* Replaces Evaluator::Plus -> Program::Plus (internal/ceres/program.cc:121-149,
  * internal/ceres/parameter_block.h:227-251) for problems whose active
- * parameter blocks have no manifold: x_plus_delta = x + delta block by block
- * (state offsets vs delta offsets of the descriptor).  Box constraints are
- * not part of the descriptor, so none are applied.  Returns
- * CSE_ERR_UNSUPPORTED when an active block has a manifold (the caller keeps
- * Ceres' host Plus for those).
+ * parameter blocks have no manifold or the quaternion manifold:
+ * x_plus_delta = x + delta block by block (state offsets vs delta offsets of
+ * the descriptor), CSE_MANIFOLD_QUATERNION_EUCLIDEAN blocks by their
+ * manifold's Plus.  Box constraints are not part of the descriptor, so none
+ * are applied.  Returns CSE_ERR_UNSUPPORTED when an active block has an
+ * explicit plus-Jacobian manifold (the caller keeps Ceres' host Plus).
  *   cse_plus_device: device pointers, asynchronous on the evaluator's stream
  *   cse_plus:        host pointers, synchronous */
 int cse_plus_device(cse_evaluator* ev, const double* d_state, const double* d_delta,

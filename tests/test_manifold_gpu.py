@@ -135,3 +135,54 @@ def test_problem_13682_quaternion_manifold(gpu):
     rep = {}
     assert_parity(got, ref, "problem-13682 quaternion manifold", report=rep)
     print("problem-13682 quaternion-manifold parity:", rep)
+
+
+def quaternion_plus_reference(x, delta):
+    """ProductManifold<QuaternionManifold, EuclideanManifold<n>>::Plus as
+    QuaternionPlusImpl (internal/ceres/manifold.cc:28-59) states it."""
+    out = x.copy()
+    d = delta[:3]
+    nd = np.sqrt((d * d).sum())
+    if nd != 0.0:
+        s = np.sin(nd) / nd
+        w, a, b, c = np.cos(nd), s * d[0], s * d[1], s * d[2]
+        q = x[:4]
+        out[0] = w * q[0] - a * q[1] - b * q[2] - c * q[3]
+        out[1] = w * q[1] + a * q[0] + b * q[3] - c * q[2]
+        out[2] = w * q[2] - a * q[3] + b * q[0] + c * q[1]
+        out[3] = w * q[3] + a * q[2] - b * q[1] + c * q[0]
+    out[4:] = x[4:] + delta[3:]
+    return out
+
+
+def test_plus_on_the_quaternion_manifold(gpu):
+    """cse_plus: quaternion cameras by QuaternionPlusImpl (zero rotation
+    steps included), points by x + delta."""
+    prog = quat_program(seed=17)
+    P, C = 700, 16
+    rng = np.random.default_rng(5)
+    delta = rng.normal(0.0, 1e-3, prog.num_effective_parameters)
+    delta[3 * P: 3 * P + 3] = 0.0  # camera 0: no rotation step
+    ev = ca.Evaluator(prog)
+    got = ev.plus(prog.state, delta)
+    ev.close()
+    want = np.empty_like(prog.state)
+    want[:3 * P] = prog.state[:3 * P] + delta[:3 * P]
+    for c in range(C):
+        so, do = 3 * P + 10 * c, 3 * P + 9 * c
+        want[so:so + 10] = quaternion_plus_reference(prog.state[so:so + 10], delta[do:do + 9])
+    assert np.array_equal(got[:3 * P], want[:3 * P])
+    assert np.array_equal(got[3 * P:3 * P + 10], want[3 * P:3 * P + 10])  # zero step: exact
+    assert np.allclose(got, want, rtol=1e-14, atol=1e-15)
+
+
+def test_bundle_adjuster_with_quaternion_manifolds(gpu):
+    """bundle_adjuster --use_quaternions --use_manifolds: evaluations, Plus on
+    the manifold and the iterative Schur solve all on the device."""
+    from ceres_amd import bundle_adjuster
+    c0, c1, rows = bundle_adjuster.main(["--synthetic", "problem-16-22106", "--robustify",
+                                         "--use_quaternions", "--use_manifolds",
+                                         "--point_sigma", "0.05", "--num_iterations", "4"])
+    assert c1 < 0.9 * c0
+    costs = [r[1] for r in rows] + [c1]
+    assert all(b <= a for a, b in zip(costs, costs[1:]))
