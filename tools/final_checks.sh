@@ -6,7 +6,7 @@ export CSE_BAL_CACHE=/tmp/cse_bal_cache
 OUT=gpurun_out/final
 mkdir -p $OUT
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || { echo "pytest rc=$?"; tail -20 $OUT/pytest_gpu.txt; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --durations=15 --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || { echo "pytest rc=$?"; tail -20 $OUT/pytest_gpu.txt; exit 1; }
 tail -2 $OUT/pytest_gpu.txt
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
 cut -c1-300 $OUT/bench.json
