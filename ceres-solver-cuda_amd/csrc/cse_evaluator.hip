@@ -402,6 +402,7 @@ LaunchFn TuningVariant(int v, bool jac) {
       case 60: return &LaunchResidualStreamed<K, L, 8, 2>;
       case 61: return &LaunchResidualStreamed<K, L, 16, 1>;
       case 62: return &LaunchResidualStreamed<K, L, 4, 4>;
+      case 63: return &LaunchChunks<K, L, false, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 0, 0, false, true>>;
       default: return nullptr;
     }
   }
@@ -437,6 +438,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 34: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 1>, 4>;
     case 35: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 3, 3, 3>, 4>;
     case 36: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 4, 4, 4>, 4>;
+    // XCD-contiguous workgroup ranges (Tune::kXcdMap) on the shipped kernel
+    case 37: return &LaunchBounded<K, L, true, false, 2, cse::Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 0, 0, false, true>, 4>;
     // persistent wave-specialised pipeline, 4 / 3 / 2 store waves
     case 40: return &LaunchPipelined<K, L, 4>;
     case 41: return &LaunchPipelined<K, L, 3>;

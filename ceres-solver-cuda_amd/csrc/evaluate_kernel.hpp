@@ -509,7 +509,8 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
 template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
           int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
-          int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0, bool kConst0_ = false>
+          int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0, bool kConst0_ = false,
+          bool kXcdMap_ = false>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -527,7 +528,18 @@ struct Tune {
   static constexpr int kRPol = kRPol_;  // and of the residual stores
   static constexpr int kFPol = kFPol_;  // and of the F-cell stores
   static constexpr bool kConst0 = kConst0_;  // constant slot-0 blocks (BSM)
+  // Workgroups dispatched round-robin over the 8 XCDs get contiguous chunk
+  // ranges per XCD (workgroup b -> XCD b % 8, remapped to a bijection).
+  static constexpr bool kXcdMap = kXcdMap_;
 };
+
+// The logical workgroup of dispatch index b when each of the 8 XCDs is to
+// take one contiguous range of the grid (round-robin dispatch: b -> XCD
+// b % 8): XCD x owns [x*q + min(x, r), ...) of q + (x < r) workgroups.
+__device__ __forceinline__ int64_t XcdContiguous(int64_t b, int64_t nwg) {
+  const int64_t x = b & 7, k = b >> 3, q = nwg >> 3, r = nwg & 7;
+  return x * q + (x < r ? x : r) + k;
+}
 // Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
 // sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
 // functor's FP64 work shrank, s3d); two-round E/F staging (9 KiB of LDS a
@@ -584,7 +596,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
-  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t wg = T::kXcdMap ? XcdContiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t c = wg * kWavesPerBlock + wave;
   double* partial_dst = a.partials + c;
   if (c >= num_chunks) {
     if (lane == 0) *partial_dst = 0.0;  // the group's partial slots are 4 per workgroup
