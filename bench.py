@@ -427,6 +427,13 @@ def main():
                 "point rows fused into the evaluation, camera rows re-evaluated in camera "
                 "order; what TrustRegionMinimizer requests); bytes add 8 per "
                 "effective parameter")
+        leg("same_point", lambda: se.evaluate(residuals=True, jacobian=True, gradient=False,
+                                              new_evaluation_point=False),
+            info.bytes_jacobian_eval, ks,
+            "the headline evaluation with new_evaluation_point = false (CSE_EVAL_SAME_POINT), "
+            "as TrustRegionMinimizer evaluates the Jacobian at a just-accepted candidate "
+            "(trust_region_minimizer.cc:822-826): the slot-0 table repacked for that point "
+            "by the candidate's evaluation is reused")
         leg("residual_only", lambda: se.evaluate(residuals=True, jacobian=False, gradient=False),
             info.bytes_residual_eval, ks, "residuals + cost (trust-region candidate evaluation)")
         hres, hjac = se.host_buffers()

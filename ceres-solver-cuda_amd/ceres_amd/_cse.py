@@ -19,6 +19,7 @@ CSE_ERR_INVALID = -1
 CSE_ERR_HIP = -2
 CSE_ERR_OOM = -3
 CSE_ERR_UNSUPPORTED = -4
+EVAL_SAME_POINT = 1  # CSE_EVAL_SAME_POINT: new_evaluation_point == false
 
 # cse_functor_kind
 SNAVELY_2_9_3 = 0
@@ -134,6 +135,9 @@ SIGNATURES = {
     "cse_evaluate": (C.c_int, [C.c_void_p, P_f64, P_f64, P_f64, P_f64, P_f64]),
     "cse_evaluate_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p]),
+    "cse_evaluate_ex": (C.c_int, [C.c_void_p, P_f64, P_f64, P_f64, P_f64, P_f64, C.c_uint32]),
+    "cse_evaluate_device_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_uint32]),
     "cse_wait": (C.c_int, [C.c_void_p]),
     "cse_set_plus_jacobians": (C.c_int, [C.c_void_p, P_f64]),
     "cse_plus_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -164,6 +168,10 @@ SIGNATURES = {
     "cse_build_info": (C.c_char_p, []),
 }
 
+# Entry points an older build (tools/ A/B runs against a previous commit) may lack.
+_SINCE_ROUND3 = {"cse_evaluate_ex", "cse_evaluate_device_ex"}
+_DEFAULT_LIB = LIB_PATH
+
 _lib = None
 
 
@@ -186,6 +194,8 @@ def lib():
                 f"ceres-solver-cuda_amd` (there is no CPU fallback)")
         handle = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if name in _SINCE_ROUND3 and LIB_PATH != _DEFAULT_LIB and not hasattr(handle, name):
+                continue  # an older build loaded for an A/B (tools/)
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

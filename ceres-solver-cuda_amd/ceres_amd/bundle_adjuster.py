@@ -123,9 +123,12 @@ def solve(args):
         timers.add(name, time.perf_counter() - s)
         return out
 
-    def jacobian_eval():
+    def jacobian_eval(new_point=True):
+        # After an accepted step x holds the candidate just evaluated:
+        # new_evaluation_point = false, as HandleSuccessfulStep passes
+        # (trust_region_minimizer.cc:822-826).
         ev.evaluate_device(x.data_ptr(), cost.data_ptr(), r.data_ptr(), g.data_ptr(),
-                           jac.data_ptr())
+                           jac.data_ptr(), new_evaluation_point=new_point)
         return ev.wait()
 
     def normal_op(v, sqrt_lam_d):
@@ -252,7 +255,7 @@ def solve(args):
                      radius, cg_iters, accepted))
         if accepted:
             x.copy_(cand)
-            if timed("Jacobian & residual evaluation", jacobian_eval) != 0:
+            if timed("Jacobian & residual evaluation", lambda: jacobian_eval(False)) != 0:
                 raise SystemExit(f"iteration {it}: Jacobian evaluation at the accepted point failed")
             d_stale = True
             radius = min(max_radius, radius / max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3))

@@ -77,7 +77,8 @@ class ShardedEvaluator:
         self._pending = []
 
     # ---- evaluation -------------------------------------------------------
-    def evaluate(self, residuals=True, jacobian=True, gradient=None, cost=None, overlap=False):
+    def evaluate(self, residuals=True, jacobian=True, gradient=None, cost=None, overlap=False,
+                 new_evaluation_point=True):
         """One Evaluate of this rank's shard, then the exchange step.
 
         The evaluation is asynchronous on the rank's stream.  The cost goes to
@@ -88,7 +89,8 @@ class ShardedEvaluator:
         the next evaluation proceeds; its handle is kept until
         wait_exchange(), so each call must pass its own `cost` buffer.  The
         gradient's camera rows are always reduced in order (the gradient
-        buffer is shared)."""
+        buffer is shared).  new_evaluation_point=False: the state
+        equals the previous evaluation's (CSE_EVAL_SAME_POINT)."""
         gradient = self.gradient is not None if gradient is None else gradient
         if gradient and self.gradient is None:
             raise ValueError("ShardedEvaluator built without a gradient buffer")
@@ -97,7 +99,8 @@ class ShardedEvaluator:
         self.evaluator.evaluate_device(self.state.data_ptr(), cost.data_ptr(),
                                        ptr(self.residuals, residuals),
                                        ptr(self.gradient, gradient),
-                                       ptr(self.jacobian, jacobian))
+                                       ptr(self.jacobian, jacobian),
+                                       new_evaluation_point=new_evaluation_point)
         if self.exchange:
             # The collectives are ordered against the evaluation's stream: a
             # collective (and gloo's host copy) follows torch's current

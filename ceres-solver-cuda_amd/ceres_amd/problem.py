@@ -472,10 +472,13 @@ class Evaluator:
                                     _ptr(devs, C.c_int32)), "cse_shard_info")
         return first, devs
 
-    def evaluate(self, state=None, residuals=True, gradient=True, jacobian=True, out=None):
+    def evaluate(self, state=None, residuals=True, gradient=True, jacobian=True, out=None,
+                 new_evaluation_point=True):
         """Host-pointer Evaluate.  Returns (ok, cost, residuals, gradient, jacobian).
         out: optional (r, g, j) float64 arrays to write into (None entries are
-        allocated), e.g. buffers kept across calls."""
+        allocated), e.g. buffers kept across calls.  new_evaluation_point=False:
+        the state equals the previous evaluation's (Evaluator::EvaluateOptions,
+        evaluator.h:106-107; cse_evaluate_ex with CSE_EVAL_SAME_POINT)."""
         p = self.program
         state = np.ascontiguousarray(p.state if state is None else state, np.float64)
         cost = C.c_double(-1.0)
@@ -483,15 +486,23 @@ class Evaluator:
         r = (ro if ro is not None else np.empty(p.num_residuals)) if residuals else None
         g = (go if go is not None else np.empty(p.num_effective_parameters)) if gradient else None
         j = (jo if jo is not None else np.empty(p.num_jacobian_values)) if jacobian else None
-        rc = _cse.lib().cse_evaluate(self.handle, _ptr(state, C.c_double), C.byref(cost),
-                                     _ptr(r, C.c_double), _ptr(g, C.c_double), _ptr(j, C.c_double))
+        flags = 0 if new_evaluation_point else _cse.EVAL_SAME_POINT
+        rc = _cse.lib().cse_evaluate_ex(self.handle, _ptr(state, C.c_double), C.byref(cost),
+                                        _ptr(r, C.c_double), _ptr(g, C.c_double),
+                                        _ptr(j, C.c_double), flags)
         _cse.check(rc, "cse_evaluate")
         return rc == _cse.CSE_OK, cost.value, r, g, j
 
-    def evaluate_device(self, d_state, d_cost, d_residuals=None, d_gradient=None, d_jacobian=None):
-        """Device-pointer Evaluate (integers = device addresses).  Async."""
-        rc = _cse.lib().cse_evaluate_device(self.handle, d_state, d_cost, d_residuals, d_gradient,
-                                            d_jacobian)
+    def evaluate_device(self, d_state, d_cost, d_residuals=None, d_gradient=None, d_jacobian=None,
+                        new_evaluation_point=True):
+        """Device-pointer Evaluate (integers = device addresses).  Async.
+        new_evaluation_point=False: CSE_EVAL_SAME_POINT (see evaluate)."""
+        if new_evaluation_point:
+            rc = _cse.lib().cse_evaluate_device(self.handle, d_state, d_cost, d_residuals,
+                                                d_gradient, d_jacobian)
+        else:
+            rc = _cse.lib().cse_evaluate_device_ex(self.handle, d_state, d_cost, d_residuals,
+                                                   d_gradient, d_jacobian, _cse.EVAL_SAME_POINT)
         return _cse.check(rc, "cse_evaluate_device")
 
     def wait(self):

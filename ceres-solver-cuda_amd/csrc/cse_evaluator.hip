@@ -569,6 +569,11 @@ struct cse_evaluator {
   DevBuf<double> h_state, h_cost, h_res, h_jac, h_grad;
   DevBuf<double> cg_z;  // cse_cgnr_multiply's z = J x when it cannot fuse
   int* status_host = nullptr;  // pinned
+  // Evaluate at the same point (CSE_EVAL_SAME_POINT): the packed slot-0
+  // tables hold the state of the last evaluation queued without error, and
+  // h_state the last host state uploaded (cleared by a device-pointer call).
+  bool point_current = false;
+  bool host_state_current = false;
   // Profiling: one (start, stop) event pair per evaluation around its
   // group kernels, folded lazily so timing never stalls the launch queue.
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
@@ -1133,16 +1138,24 @@ int BuildSchurPlan(cse_evaluator* ev, const cse_problem_desc* d, hipStream_t s) 
 }
 
 // Enqueue one evaluation on ev->stream.
+// same_point (CSE_EVAL_SAME_POINT): the state equals the previous
+// evaluation's, so the packed slot-0 tables it built are still valid and the
+// repack launches are skipped.
 int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_res,
-            double* d_grad, double* d_jac) {
+            double* d_grad, double* d_jac, bool same_point = false) {
   if (d_jac && !ev->has_layout)
     return Fail(CSE_ERR_INVALID, "Jacobian requested but the descriptor had no Jacobian layout");
+  const bool repack = !(same_point && ev->point_current);
+  ev->point_current = false;  // set again once every launch below is queued
   const bool jets = d_jac || d_grad;
   std::pair<hipEvent_t, hipEvent_t> timing{nullptr, nullptr};
   if (ev->opts.profile) {
     if (ev->pool.empty()) {
-      CSE_HIP(hipEventCreate(&timing.first));
-      CSE_HIP(hipEventCreate(&timing.second));
+      // Timing only: no system-scope fence (cache write-back and
+      // invalidation) at either event, which cost ~7-10 us per evaluation
+      // at the 8-way shard and problem-16 (profiles/round3/ov0).
+      CSE_HIP(hipEventCreateWithFlags(&timing.first, hipEventDisableSystemFence));
+      CSE_HIP(hipEventCreateWithFlags(&timing.second, hipEventDisableSystemFence));
     } else {
       timing = ev->pool.back();
       ev->pool.pop_back();
@@ -1189,7 +1202,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       fn = PickFused(G.kind, G.loss.kind, G.policy, recompute, G.const0);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
-    if (dma) {
+    if (dma && repack) {
       const int pieces = (G.shape.x0 + 1) / 2;
       const int64_t total = G.slot0_count * pieces;
       hipLaunchKernelGGL(cse::RepackSlot0Kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
@@ -1245,6 +1258,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
                        d_cost, ev->status.p, ev->status.p + 1);
   }
   CSE_HIP(hipGetLastError());
+  ev->point_current = true;
   return CSE_OK;
 }
 
@@ -1548,13 +1562,22 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   return CSE_OK;
 }
 
-int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost,
-                        double* d_residuals, double* d_gradient, double* d_jacobian_values) {
+int cse_evaluate_device_ex(cse_evaluator* ev, const double* d_state, double* d_cost,
+                           double* d_residuals, double* d_gradient, double* d_jacobian_values,
+                           uint32_t flags) {
   if (!ev || !d_cost) return Fail(CSE_ERR_INVALID, "null evaluator or cost");
   CSE_SINGLE_DEVICE(ev, "cse_evaluate_device");
+  if (flags & ~(uint32_t)CSE_EVAL_SAME_POINT) return Fail(CSE_ERR_INVALID, "unknown evaluate flags");
   if (ev->num_parameters > 0 && !d_state) return Fail(CSE_ERR_INVALID, "null state");
   if (hipSetDevice(ev->device) != hipSuccess) return Fail(CSE_ERR_HIP, "hipSetDevice failed");
-  return Enqueue(ev, d_state, d_cost, d_residuals, d_gradient, d_jacobian_values);
+  ev->host_state_current = false;
+  return Enqueue(ev, d_state, d_cost, d_residuals, d_gradient, d_jacobian_values,
+                 (flags & CSE_EVAL_SAME_POINT) != 0);
+}
+
+int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost,
+                        double* d_residuals, double* d_gradient, double* d_jacobian_values) {
+  return cse_evaluate_device_ex(ev, d_state, d_cost, d_residuals, d_gradient, d_jacobian_values, 0);
 }
 
 int cse_wait(cse_evaluator* ev) {
@@ -1570,12 +1593,14 @@ int cse_wait(cse_evaluator* ev) {
   return *ev->status_host ? CSE_EVALUATION_FAILED : CSE_OK;
 }
 
-int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* residuals,
-                 double* gradient, double* jacobian_values) {
+int cse_evaluate_ex(cse_evaluator* ev, const double* state, double* cost, double* residuals,
+                    double* gradient, double* jacobian_values, uint32_t flags) {
   if (!ev || !cost) return Fail(CSE_ERR_INVALID, "null evaluator or cost");
+  if (flags & ~(uint32_t)CSE_EVAL_SAME_POINT) return Fail(CSE_ERR_INVALID, "unknown evaluate flags");
+  const bool same_point = (flags & CSE_EVAL_SAME_POINT) != 0;
   if (ev->multi) {
     if (!state) return Fail(CSE_ERR_INVALID, "null state");
-    return MultiEvaluate(ev->multi, state, cost, residuals, gradient, jacobian_values);
+    return MultiEvaluate(ev->multi, state, cost, residuals, gradient, jacobian_values, same_point);
   }
   if (ev->num_parameters > 0 && !state) return Fail(CSE_ERR_INVALID, "null state");
   CSE_HIP(hipSetDevice(ev->device));
@@ -1587,12 +1612,18 @@ int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* r
   if (jacobian_values && !ev->h_jac.p &&
       (rc = ev->h_jac.alloc(std::max<int64_t>(ev->num_jacobian_values, 1))))
     return rc;
-  if (ev->num_parameters > 0)
+  // At the same point the state uploaded for the previous host-pointer
+  // evaluation is still in h_state (Evaluator::EvaluateOptions::
+  // new_evaluation_point == false, trust_region_minimizer.cc:826).
+  if (ev->num_parameters > 0 && !(same_point && ev->host_state_current)) {
+    ev->host_state_current = false;
     CSE_HIP(hipMemcpyAsync(ev->h_state.p, state, ev->num_parameters * sizeof(double),
                            hipMemcpyHostToDevice, ev->stream));
+  }
   rc = Enqueue(ev, ev->h_state.p, ev->h_cost.p, residuals ? ev->h_res.p : nullptr,
-               gradient ? ev->h_grad.p : nullptr, jacobian_values ? ev->h_jac.p : nullptr);
+               gradient ? ev->h_grad.p : nullptr, jacobian_values ? ev->h_jac.p : nullptr, same_point);
   if (rc) return rc;
+  ev->host_state_current = true;
   rc = cse_wait(ev);
   if (rc < 0) return rc;
   if (rc == CSE_EVALUATION_FAILED) return rc;
@@ -1605,6 +1636,11 @@ int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* r
     CSE_HIP(hipMemcpy(jacobian_values, ev->h_jac.p, ev->num_jacobian_values * sizeof(double),
                       hipMemcpyDeviceToHost));
   return CSE_OK;
+}
+
+int cse_evaluate(cse_evaluator* ev, const double* state, double* cost, double* residuals,
+                 double* gradient, double* jacobian_values) {
+  return cse_evaluate_ex(ev, state, cost, residuals, gradient, jacobian_values, 0);
 }
 
 int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians) {

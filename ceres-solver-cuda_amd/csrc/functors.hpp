@@ -63,22 +63,27 @@ CSE_HD void RodriguesFactors(const Jet<N>& u, Jet<N>* s, Jet<N>* c) {
 // from theta == 0, the first-order form R = I + hat(w) exactly at zero so
 // Jets still carry the right derivatives.
 //
-// On the device, when every lane of the wave has theta^2 <= 1 (rotations of
-// up to 57 degrees, the usual BAL camera; a wave-uniform ballot, so no wave
-// runs both forms), the same rotation is evaluated as
+// On the device, a lane whose theta^2 <= 1 (rotations of up to 57 degrees,
+// the usual BAL camera) evaluates the same rotation as
 //   R x = x + s(theta^2) (w x x) + c(theta^2) (w x (w x x)),  w = angle_axis,
 // Rodrigues' formula with sin(theta)/theta and (1 - cos(theta))/theta^2 as
 // series in theta^2 (RodriguesFactors): no square root, no division, no
 // sine or cosine, and the cross products of the seeded Jets carry their
 // partials as plain copies.  At theta == 0 it is exactly the reference's
 // first-order form (s = 1, c = 1/2, and the c term vanishes with its
-// derivatives), so both branches of the reference are covered.
+// derivatives), so both branches of the reference are covered.  The form is
+// chosen per lane, from the block's own camera: a block's outputs do not
+// depend on which blocks share its wave (a sharded evaluation writes the
+// same bits as the whole-problem one, and the camera-order gradient
+// re-evaluation takes the same form as the point-order evaluation).  A wave
+// whose lanes all fall on one side runs that form alone (the other is
+// skipped on an empty exec mask); a mixed wave runs both.
 template <typename T>
 CSE_HD void AngleAxisRotatePoint(const T aa[3], const T pt[3], T out[3]) {
 #ifdef __HIP_DEVICE_COMPILE__
   {
     const T u = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
-    if (__builtin_amdgcn_ballot_w64(!(value_of(u) <= 1.0)) == 0) {
+    if (value_of(u) <= 1.0) {
       T s, c;
       RodriguesFactors(u, &s, &c);
       const T q[3] = {aa[1] * pt[2] - aa[2] * pt[1],

@@ -144,9 +144,9 @@ template <int N> CSE_HD Jet<N> jabs(const Jet<N>& f) {
 // no range reduction is needed and both come from the minimax polynomials of
 // fdlibm's __kernel_sin / __kernel_cos (error below 1 ulp on [-pi/4, pi/4]):
 // about 22 FP64 operations against about 50 for the library sincos, whose
-// reduction step is an identity there.  The test is wave-uniform (a ballot),
-// so a wave with any larger angle takes the library path for all lanes and
-// never runs both.
+// reduction step is an identity there.  The test is per lane, so a lane's
+// result depends only on its own argument (a wave whose lanes all fall on one
+// side runs that path alone).
 CSE_HD void SinCosSmall(double x, double* s, double* c) {
   const double z = x * x, w = z * z;
   const double rs = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 +
@@ -162,7 +162,7 @@ CSE_HD void SinCosSmall(double x, double* s, double* c) {
 }
 CSE_HD void SinCos(double x, double* s, double* c) {
 #ifdef __HIP_DEVICE_COMPILE__
-  if (__builtin_amdgcn_ballot_w64(!(fabs(x) <= 0.78539816339744828)) == 0) {
+  if (fabs(x) <= 0.78539816339744828) {
     SinCosSmall(x, s, c);
     return;
   }

@@ -32,7 +32,7 @@ int MultiCreate(const cse_problem_desc* desc, const cse_options* options, const 
                 int32_t num_devices, CseMulti** out);
 void MultiDestroy(CseMulti* m);
 int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residuals,
-                  double* gradient, double* jacobian_values);
+                  double* gradient, double* jacobian_values, bool same_point);
 int MultiInfo(CseMulti* m, cse_info* info);
 int MultiShardInfo(CseMulti* m, int32_t* num_shards, int64_t* first_block, int32_t* devices);
 int MultiSetPlusJacobians(CseMulti* m, const double* plus_jacobians);

@@ -120,6 +120,9 @@ struct CseMulti {
   int64_t num_parameters = 0, num_effective = 0, num_residuals = 0, num_jacobian_values = 0;
   int64_t num_residual_blocks = 0;
   bool has_layout = false;
+  // Every shard's d_state holds the state of the last evaluation queued
+  // without error (CSE_EVAL_SAME_POINT skips the copies).
+  bool state_current = false;
   // The caller's host buffers, page-locked on first use (one per role).
   struct Reg {
     void* p = nullptr;
@@ -415,7 +418,7 @@ void MultiDestroy(CseMulti* m) {
 }
 
 int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residuals,
-                  double* gradient, double* jac) {
+                  double* gradient, double* jac, bool same_point) {
   if (jac && !m->has_layout)
     return CseFail(CSE_ERR_INVALID, "Jacobian requested but the descriptor had no Jacobian layout");
   const bool async_state = Register(m, 0, state, m->num_parameters * sizeof(double));
@@ -423,17 +426,20 @@ int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residu
   const bool async_jac = jac && Register(m, 2, jac, m->num_jacobian_values * sizeof(double));
   // Queue every shard: state H2D, evaluation, strips D2H (disjoint regions of
   // the caller's buffers), gradient rows and cost into pinned staging.
+  const bool copy_state = !(same_point && m->state_current);
+  m->state_current = false;
   for (auto& s : m->shards) {
     MD_HIP(hipSetDevice(s.device));
-    if (m->num_parameters > 0) {
+    if (m->num_parameters > 0 && copy_state) {
       if (async_state)
         MD_HIP(hipMemcpyAsync(s.d_state, state, m->num_parameters * sizeof(double),
                               hipMemcpyHostToDevice, s.stream));
       else
         MD_HIP(hipMemcpy(s.d_state, state, m->num_parameters * sizeof(double), hipMemcpyHostToDevice));
     }
-    int rc = cse_evaluate_device(s.ev, s.d_state, s.d_cost, residuals ? s.d_res : nullptr,
-                                 gradient ? s.d_grad : nullptr, jac ? s.d_jac : nullptr);
+    int rc = cse_evaluate_device_ex(s.ev, s.d_state, s.d_cost, residuals ? s.d_res : nullptr,
+                                    gradient ? s.d_grad : nullptr, jac ? s.d_jac : nullptr,
+                                    same_point ? CSE_EVAL_SAME_POINT : 0u);
     if (rc) return rc;
     MD_HIP(hipMemcpyAsync(s.h_cost, s.d_cost, sizeof(double), hipMemcpyDeviceToHost, s.stream));
     if (residuals && async_res)
@@ -449,6 +455,7 @@ int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residu
         MD_HIP(hipMemcpyAsync(s.h_grad + iv.local, s.d_grad + iv.begin,
                               (iv.end - iv.begin) * sizeof(double), hipMemcpyDeviceToHost, s.stream));
   }
+  m->state_current = true;
   // Wait for every shard (cse_wait synchronises the shard's stream, which
   // carries the copies too) and collect the statuses.
   int status = CSE_OK;

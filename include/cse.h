@@ -225,6 +225,26 @@ int cse_evaluate_device(cse_evaluator* ev, const double* d_state, double* d_cost
                         double* d_residuals, double* d_gradient,
                         double* d_jacobian_values);
 
+/* Evaluate flags.  CSE_EVAL_SAME_POINT carries
+ * Evaluator::EvaluateOptions::new_evaluation_point == false
+ * (internal/ceres/evaluator.h:106-107): the state has the same values as at
+ * the previous evaluation on this evaluator, as when TrustRegionMinimizer
+ * evaluates the Jacobian at a just-accepted candidate
+ * (trust_region_minimizer.cc:822-826).  The library then reuses what it
+ * derived from the state last time: the state already copied to the device
+ * (cse_evaluate_ex, the multi-device evaluator) and the repacked slot-0
+ * table of the affine kernels.  The state pointer may differ; its values
+ * must not.  Ignored when there is no previous evaluation to reuse. */
+#define CSE_EVAL_SAME_POINT 1u
+
+/* cse_evaluate / cse_evaluate_device with flags (0 = the plain call). */
+int cse_evaluate_ex(cse_evaluator* ev, const double* state, double* cost,
+                    double* residuals, double* gradient, double* jacobian_values,
+                    uint32_t flags);
+int cse_evaluate_device_ex(cse_evaluator* ev, const double* d_state, double* d_cost,
+                           double* d_residuals, double* d_gradient,
+                           double* d_jacobian_values, uint32_t flags);
+
 /* Synchronises the evaluator's stream and returns the status of the most
  * recent evaluation (CSE_OK / CSE_EVALUATION_FAILED) or an error. */
 int cse_wait(cse_evaluator* ev);

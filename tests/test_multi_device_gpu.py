@@ -114,6 +114,47 @@ def test_multi_device_multiple_groups_and_table_path(gpu):
         assert_parity(got, ref, ("multi mini-BA", fmt))
 
 
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+def test_shard_strips_bit_identical_to_the_whole_problem(gpu, fmt):
+    """A block's residuals and Jacobian do not depend on which blocks share
+    its wave: the rotation form (series or the reference's) is chosen per
+    lane (csrc/functors.hpp AngleAxisRotatePoint), so the strips of 8
+    per-rank shards -- whose waves start at other blocks -- carry the same
+    bits as the whole-problem evaluation.  Camera angles are mixed (about one
+    camera in eight beyond theta^2 = 1, and tiny and zero angles), so many
+    waves mix the two forms."""
+    C, P = 40, 5000
+    cams, pts, ci, pi, obs = bal.synthetic(C, P, 30011, seed=21)
+    rng = np.random.default_rng(21)
+    axis = rng.normal(size=(C, 3))
+    axis /= np.linalg.norm(axis, axis=1)[:, None]
+    theta = np.where(rng.random(C) < 0.125, rng.uniform(1.0, 3.0, C), rng.uniform(0.0, 1.0, C))
+    theta[:3] = [0.0, 2.0 ** -30, 1.0 + 2.0 ** -52]
+    cams = cams.copy()
+    cams[:, 0:3] = axis * theta[:, None]
+    obs = bal.project(cams, pts, ci, pi) + rng.normal(0.0, 1.0, (len(ci), 2))
+    loss = ca.Loss.huber(1.0)
+    full = bal.program(cams, pts, ci, pi, obs, loss=loss, format=fmt)
+    ev = ca.Evaluator(full, device=0)
+    ok, _, R, _, J = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    ev.close()
+    assert ok
+    world = 8
+    shards, jparts = [], []
+    for rank in range(world):
+        prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss, format=fmt)
+        ev = ca.Evaluator(prog, device=0)
+        ok, _, r, _, j = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+        ev.close()
+        assert ok
+        r0, r1 = sh.residual_strip
+        assert np.array_equal(r, R[r0:r1]), (fmt, rank)
+        shards.append(sh)
+        jparts.append(j)
+    Js = shard.assemble(shards, jparts, full.num_jacobian_values)
+    assert np.array_equal(Js, J), fmt
+
+
 def test_multi_device_refuses_device_pointer_calls(gpu):
     prog = bal.synthetic_program((8, 300, 1200), seed=2)
     ev = ca.Evaluator(prog, devices=[0, 0])
