@@ -574,6 +574,11 @@ struct cse_evaluator {
   // h_state the last host state uploaded (cleared by a device-pointer call).
   bool point_current = false;
   bool host_state_current = false;
+  // gradient_mode 0: CameraGradientKernel runs on a second stream beside the
+  // points kernel (created on first use), forked after the repack and joined
+  // before the camera rows are written.
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   // Profiling: one (start, stop) event pair per evaluation around its
   // group kernels, folded lazily so timing never stalls the launch queue.
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
@@ -995,9 +1000,9 @@ int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
 
 // gradient_mode 0: the slot-1 boundary entries as above, and the slot-0
 // sums by re-evaluation in camera order (CameraGradientKernel), then
-// GradientChunkReduceKernel.  The sorted inputs are built on first use.
-int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, double* out,
-                         hipStream_t s) {
+// GradientChunkReduceKernel.  The sorted inputs are built on first use
+// (CamGradSortedInputs, on the evaluator's stream, before the fork).
+int CamGradSortedInputs(Group& G, hipStream_t s) {
   const Group::GradPlan& P = G.grad[0];
   const int D = G.shape.data;
   int rc;
@@ -1012,10 +1017,12 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
     CSE_HIP(hipGetLastError());
     G.sorted_ready = true;
   }
-  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
-  hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
-                     dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                     dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
+  return CSE_OK;
+}
+
+// CameraGradientKernel: the per-chunk slot-0 sums into P.chunk_partial.
+int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hipStream_t s) {
+  const Group::GradPlan& P = G.grad[0];
   cse::CamGradArgs cg{};
   cg.state = state;
   cg.state_base0 = G.state_base[0];
@@ -1056,6 +1063,18 @@ int LaunchCameraGradTail(cse_evaluator* ev, Group& G, const double* state, doubl
     if (G.kind == kKindQuaternionTangent) launch(cse::SnavelyQuaternionTangentKind{});
     else launch(cse::SnavelyKind{});
   }
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+// After the points kernel and CameraGradientKernel: the slot-1 boundary
+// entries, then the slot-0 rows from the chunk sums, in a fixed order.
+int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s) {
+  const Group::GradPlan& P = G.grad[0];
+  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
+  hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
+                     dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                     dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
   cse::GradArgs ga{};
   ga.count = P.count;
   ga.lo = P.lo;
@@ -1138,6 +1157,33 @@ int BuildSchurPlan(cse_evaluator* ev, const cse_problem_desc* d, hipStream_t s) 
 }
 
 // Enqueue one evaluation on ev->stream.
+// Where CameraGradientKernel runs: 0 (shipped) after the points kernel on
+// the evaluator's stream; 1 on a second stream beside it (measured 3.9 %
+// slower, 2.23 vs 2.15 ms: profiles/round3/s2); 2 on a second,
+// low-priority stream, queued behind the points kernel (A/B builds only).
+#ifndef CSE_GRAD_CONCURRENT
+#define CSE_GRAD_CONCURRENT 0
+#endif
+constexpr bool kGradConcurrent = CSE_GRAD_CONCURRENT != 0;
+
+int EnsureSideStream(cse_evaluator* ev) {
+  int least = 0, greatest = 0;
+  if (CSE_GRAD_CONCURRENT == 2) (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (!ev->side && hipStreamCreateWithPriority(&ev->side, hipStreamNonBlocking, least) != hipSuccess) {
+    ev->side = nullptr;
+    return Fail(CSE_ERR_HIP, "side stream creation failed");
+  }
+  if (!ev->fork && hipEventCreateWithFlags(&ev->fork, hipEventDisableTiming) != hipSuccess) {
+    ev->fork = nullptr;
+    return Fail(CSE_ERR_HIP, "event creation failed");
+  }
+  if (!ev->join && hipEventCreateWithFlags(&ev->join, hipEventDisableTiming) != hipSuccess) {
+    ev->join = nullptr;
+    return Fail(CSE_ERR_HIP, "event creation failed");
+  }
+  return CSE_OK;
+}
+
 // same_point (CSE_EVAL_SAME_POINT): the state equals the previous
 // evaluation's, so the packed slot-0 tables it built are still valid and the
 // repack launches are skipped.
@@ -1209,11 +1255,39 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
                          ev->stream, d_state, G.state_base[0], G.shape.x0, G.packed_stride, pieces,
                          G.slot0_lo, G.slot0_count, G.packed0.p, G.src0.p, ev->cstate.p);
     }
+    // gradient_mode 0: CameraGradientKernel (bound by its point-gather
+    // requests to the Infinity Cache) runs on the side stream while the
+    // points kernel (bound by HBM writes) runs here; both only read the
+    // state (and the packed table, repacked above).
+    const bool side = recompute && kGradConcurrent;
+    if (recompute) {
+      int rc;
+      if ((rc = CamGradSortedInputs(G, ev->stream))) return rc;
+      if (side) {
+        if ((rc = EnsureSideStream(ev))) return rc;
+        CSE_HIP(hipEventRecord(ev->fork, ev->stream));
+        CSE_HIP(hipStreamWaitEvent(ev->side, ev->fork, 0));
+        if (CSE_GRAD_CONCURRENT == 1) {
+          if ((rc = LaunchCameraGradKernel(ev, G, d_state, ev->side))) return rc;
+          CSE_HIP(hipEventRecord(ev->join, ev->side));
+        }
+      }
+    }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
-    if (recompute) {
-      const int rc = LaunchCameraGradTail(ev, G, d_state, d_grad, ev->stream);
+    if (side && CSE_GRAD_CONCURRENT == 2) {  // queued behind the points kernel, low priority
+      const int rc = LaunchCameraGradKernel(ev, G, d_state, ev->side);
       if (rc) return rc;
+      CSE_HIP(hipEventRecord(ev->join, ev->side));
+    }
+    if (recompute) {
+      int rc;
+      if (side) {
+        CSE_HIP(hipStreamWaitEvent(ev->stream, ev->join, 0));
+      } else if ((rc = LaunchCameraGradKernel(ev, G, d_state, ev->stream))) {
+        return rc;
+      }
+      if ((rc = LaunchCameraGradReduce(G, d_grad, ev->stream))) return rc;
     } else if (fused) {
       const int rc = LaunchFusedGradTail(G, d_grad, ev->stream);
       if (rc) return rc;
@@ -1296,7 +1370,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
                                           " is not one of 0..3"));
 
   if (ev->opts.device >= 0) {
-    if (hipSetDevice(ev->opts.device) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "hipSetDevice failed"));
+    const hipError_t e = hipSetDevice(ev->opts.device);
+    if (e != hipSuccess)
+      return bail(Fail(CSE_ERR_HIP, "hipSetDevice(" + std::to_string(ev->opts.device) +
+                                        ") failed: " + hipGetErrorString(e)));
     ev->device = ev->opts.device;
   } else {
     if (hipGetDevice(&ev->device) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "no HIP device"));
@@ -2056,6 +2133,12 @@ void cse_destroy(cse_evaluator* ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
+  if (ev->side) {
+    (void)hipStreamSynchronize(ev->side);
+    (void)hipStreamDestroy(ev->side);
+  }
+  if (ev->fork) (void)hipEventDestroy(ev->fork);
+  if (ev->join) (void)hipEventDestroy(ev->join);
   if (ev->own_stream && ev->stream) (void)hipStreamDestroy(ev->stream);
   delete ev;  // every DevBuf (groups, plans, tables, scratch) frees itself
 }

@@ -14,6 +14,8 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
 
+import torch  # noqa: E402,F401  (first: libcse then shares torch's HIP runtime)
+
 import ceres_amd as ca  # noqa: E402
 from ceres_amd import bal, shard  # noqa: E402
 
@@ -22,6 +24,9 @@ def case(label, prog, steps, same_point):
     import torch
     dev = torch.device("cuda", 0)
     f64 = torch.float64
+    torch.zeros(1, device=dev)  # initialise the runtime on the device first
+    print("devices", torch.cuda.device_count(), [l.split()[-1] for l in open("/proc/self/maps")
+                                                 if "amdhip64" in l][:1], flush=True)
     s = torch.cuda.Stream(dev)
     ev = ca.Evaluator(prog, device=0, profile=False, stream=s.cuda_stream)
     state = torch.from_numpy(prog.state).to(dev)
