@@ -243,8 +243,18 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 // The shipped BSM Jacobian kernel of two-slot kinds (4 waves per SIMD).
+// CSE_TWOROUND_W1 (A/B builds): one wave per workgroup instead of four.
+#ifndef CSE_TWOROUND_W1
+#define CSE_TWOROUND_W1 0
+#endif
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  if constexpr (CSE_TWOROUND_W1 != 0) {
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundW1<K, L, Co, T>), dim3((unsigned)chunks),
+                       dim3(cse::kWave), 0, s, a);
+    return;
+  }
   hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRound<K, L, Co, T>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }

@@ -569,8 +569,10 @@ constexpr bool kTwoRoundBsm = KindTraits<K>::S1 > 0;
 //   kCoop 2: slot 0 gathered by LDS-DMA from the repacked table;
 //         1: 8-byte pieces straight from the state.
 //   kGradF: the fused gradient (FusedGrad).
+//   kWPB: waves per workgroup (chunk c = workgroup * kWPB + wave either way,
+//         so the per-wave partials keep their slots and their order).
 template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, bool kGradF = false,
-          class T = ShippedTune>
+          class T = ShippedTune, int kWPB = kWavesPerBlock>
 __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = S0 + S1;
@@ -591,13 +593,13 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   constexpr int kStageLane0 = kCoopLane > kOutLane ? kCoopLane : kOutLane;
   constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
   constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
-  __shared__ double stage[kWavesPerBlock][kWave * kStageLane];
+  __shared__ double stage[kWPB][kWave * kStageLane];
 
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
+  const int wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
   const int64_t wg = T::kXcdMap ? XcdContiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  const int64_t c = wg * kWavesPerBlock + wave;
+  const int64_t c = wg * kWPB + wave;
   double* partial_dst = a.partials + c;
   if (c >= num_chunks) {
     if (lane == 0) *partial_dst = 0.0;  // the group's partial slots are 4 per workgroup
@@ -962,6 +964,16 @@ template <class K, int kLoss, int kCoop, class T = ShippedTune>
 __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound(const GroupArgs a) {
   static_assert(kTwoRoundBsm<K>, "two-slot kinds");
   AffineChunkBody<K, kLoss, true, false, kCoop, false, T>(a);
+}
+
+// The same with one wave per workgroup (9 KiB of LDS each, 16 per CU): each
+// wave is dispatched and retired on its own, so the CU's waves do not start
+// and reach their store tails in groups of four.
+template <class K, int kLoss, int kCoop, class T = ShippedTune>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+EvaluateAffineChunksTwoRoundW1(const GroupArgs a) {
+  static_assert(kTwoRoundBsm<K>, "two-slot kinds");
+  AffineChunkBody<K, kLoss, true, false, kCoop, false, T, 1>(a);
 }
 
 // The shipped CRS Jacobian kernel: rows staged in two half-waves (24 KiB of
