@@ -52,6 +52,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
 
+if "--lib" in sys.argv:  # A/B runs (tools/): another build of the same ABI
+    from ceres_amd import _cse  # noqa: E402
+    _cse.use_library(os.path.abspath(sys.argv[sys.argv.index("--lib") + 1]))
 import ceres_amd as ca  # noqa: E402
 from ceres_amd import bal  # noqa: E402
 
@@ -98,6 +101,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the box's CPU share ($OMP_NUM_THREADS, else the affinity mask)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
+    ap.add_argument("--lib", default=None, help="load this build of libcse.so (A/B runs)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: order each cost all-reduce before the next evaluation instead of "
                          "overlapping it (the default runs it on RCCL's stream beside the next "

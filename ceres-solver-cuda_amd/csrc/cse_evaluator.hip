@@ -219,6 +219,15 @@ struct Group {
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
 
+// Waves per workgroup of the CGNR and Schur chunk kernels (one chunk per
+// wave either way); CSE_OPERATOR_W1 (A/B builds) launches them one wave per
+// workgroup, as the Jacobian kernels are: measured slower, S x 2.363 ->
+// 2.410 ms, CGNR 2.596 -> 2.614 ms (profiles/round3/w1c).
+#ifndef CSE_OPERATOR_W1
+#define CSE_OPERATOR_W1 0
+#endif
+constexpr int kOperatorWavesPerWg = CSE_OPERATOR_W1 ? 1 : cse::kWavesPerBlock;
+
 // Cost reduction: above this many per-wave partials, kPartialBlocks
 // workgroups sum slices and the last of them finalises
 // (ReduceFinalizeKernel); below, one FinalizeKernel.
@@ -236,16 +245,34 @@ void LaunchTable(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 // The affine kernel: one 64-block chunk per wave, 4 waves per workgroup.
+// CSE_CHUNKS_W1 (A/B builds): the residual-only and cost-only forms with one
+// wave per workgroup.
+#ifndef CSE_CHUNKS_W1
+#define CSE_CHUNKS_W1 0
+#endif
 template <class K, int L, bool J, bool Crs, int Co, class T = cse::ShippedTune>
 void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, T>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
+  if constexpr (CSE_CHUNKS_W1 != 0 && !J) {
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksW1<K, L, J, Crs, Co, T>), dim3((unsigned)chunks),
+                       dim3(cse::kWave), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, T>), dim3((unsigned)num_wg),
+                       dim3(cse::kBlockThreads), 0, s, a);
+  }
 }
 
-// The shipped BSM Jacobian kernel of two-slot kinds (4 waves per SIMD).
-// CSE_TWOROUND_W1 (A/B builds): one wave per workgroup instead of four.
+// The shipped BSM Jacobian kernel of two-slot kinds (4 waves per SIMD),
+// launched with one wave per workgroup (CSE_TWOROUND_W1; 0: four, the
+// round-2 form).  Each wave is then dispatched and retired on its own, and
+// the waves of a CU stop reaching their store tails in lockstep groups of
+// four: 1.447-1.454 -> 1.422-1.427 ms in same-box A/B (profiles/round3/w1);
+// the same for the fused-gradient points kernel (CSE_FUSEDPOINTS_W1),
+// gradient evaluation 2.147-2.153 -> 2.107-2.109 ms.  The residual-only
+// kernel (8 waves per SIMD) measured +1 % that way and keeps four
+// (CSE_CHUNKS_W1 0).
 #ifndef CSE_TWOROUND_W1
-#define CSE_TWOROUND_W1 0
+#define CSE_TWOROUND_W1 1
 #endif
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
@@ -253,10 +280,10 @@ void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
     const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundW1<K, L, Co, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
-    return;
+  } else {
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRound<K, L, Co, T>), dim3((unsigned)num_wg),
+                       dim3(cse::kBlockThreads), 0, s, a);
   }
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRound<K, L, Co, T>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
 }
 
 #ifdef CSE_TUNING
@@ -285,10 +312,21 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
 
 // The shipped CRS Jacobian kernel (two half-wave staging rounds, 4 waves
 // per SIMD).
+// CRS: one wave per workgroup too (neutral in same-box A/B, 1.464-1.472 ->
+// 1.468-1.469 ms, profiles/round3/w1b; kept for one launch shape).
+#ifndef CSE_TWOROUNDCRS_W1
+#define CSE_TWOROUNDCRS_W1 1
+#endif
 template <class K, int L, int Co>
 void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrs<K, L, Co>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
+  if constexpr (CSE_TWOROUNDCRS_W1 != 0) {
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrsW1<K, L, Co>), dim3((unsigned)chunks),
+                       dim3(cse::kWave), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrs<K, L, Co>), dim3((unsigned)num_wg),
+                       dim3(cse::kBlockThreads), 0, s, a);
+  }
 }
 
 // The affine kernel with the fused gradient (Snavely groups): with the
@@ -299,10 +337,19 @@ void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   hipLaunchKernelGGL((cse::EvaluateAffineChunksFused<K, L, Crs, T>), dim3((unsigned)num_wg),
                      dim3(cse::kBlockThreads), 0, s, a);
 }
+#ifndef CSE_FUSEDPOINTS_W1
+#define CSE_FUSEDPOINTS_W1 1
+#endif
 template <class K, int L, bool Crs, class T = cse::PointsOnlyTune>
 void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs, T>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
+  if constexpr (CSE_FUSEDPOINTS_W1 != 0) {
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPointsW1<K, L, Crs, T>), dim3((unsigned)chunks),
+                       dim3(cse::kWave), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs, T>), dim3((unsigned)num_wg),
+                       dim3(cse::kBlockThreads), 0, s, a);
+  }
 }
 
 // Kinds with the fused gradient: the Snavely camera and the quaternion
@@ -1861,13 +1908,14 @@ int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const 
                                 nullptr);
     a.gside = G.gside.p;
     a.gcontrib = G.gcontrib.p;
-    const dim3 grid((unsigned)((chunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
+    constexpr int W = kOperatorWavesPerWg;
+    const dim3 grid((unsigned)((chunks + W - 1) / W));
     if (G.policy == kAffineCrs)
-      hipLaunchKernelGGL((cse::CgnrMultiplyKernel<cse::SnavelyKind, true>), grid,
-                         dim3(cse::kBlockThreads), 0, s, a, d_x, d_y);
+      hipLaunchKernelGGL((cse::CgnrMultiplyKernel<cse::SnavelyKind, true, W>), grid,
+                         dim3(W * cse::kWave), 0, s, a, d_x, d_y);
     else
-      hipLaunchKernelGGL((cse::CgnrMultiplyKernel<cse::SnavelyKind, false>), grid,
-                         dim3(cse::kBlockThreads), 0, s, a, d_x, d_y);
+      hipLaunchKernelGGL((cse::CgnrMultiplyKernel<cse::SnavelyKind, false, W>), grid,
+                         dim3(W * cse::kWave), 0, s, a, d_x, d_y);
     CSE_HIP(hipGetLastError());
     if ((rc = LaunchFusedGradTail(G, d_y, s))) return rc;
   }
@@ -1909,10 +1957,10 @@ cse::SchurArgs MakeSchurArgs(cse_evaluator* ev, const double* x, double* y) {
 
 template <int kMode>
 void LaunchSchurPass(const cse::SchurArgs& a, hipStream_t s) {
+  constexpr int W = kOperatorWavesPerWg;
   if (a.nchunks > 0)
-    hipLaunchKernelGGL((cse::SchurChunkKernel<9, kMode>),
-                       dim3((unsigned)((a.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
-                       dim3(cse::kBlockThreads), 0, s, a);
+    hipLaunchKernelGGL((cse::SchurChunkKernel<9, kMode, W>), dim3((unsigned)((a.nchunks + W - 1) / W)),
+                       dim3(W * cse::kWave), 0, s, a);
   if (a.nbig > 0)
     hipLaunchKernelGGL((cse::SchurBigKernel<9, kMode>),
                        dim3((unsigned)((a.nbig + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),

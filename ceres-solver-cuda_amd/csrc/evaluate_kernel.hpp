@@ -957,6 +957,11 @@ template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T = Shipped
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const GroupArgs a) {
   AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T>(a);
 }
+// One wave per workgroup (A/B builds, CSE_CHUNKS_W1).
+template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T = ShippedTune>
+__global__ __launch_bounds__(kWave) void EvaluateAffineChunksW1(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T, 1>(a);
+}
 
 // The shipped BSM Jacobian kernel of two-slot kinds: two-round staging (36
 // KiB of LDS a workgroup, 4 per CU) held to 4 waves per SIMD (128 VGPRs).
@@ -982,6 +987,12 @@ EvaluateAffineChunksTwoRoundW1(const GroupArgs a) {
 template <class K, int kLoss, int kCoop>
 __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRoundCrs(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, true, kCoop, false, ShippedTune>(a);
+}
+// The same with one wave per workgroup (6 KiB of LDS each).
+template <class K, int kLoss, int kCoop>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+EvaluateAffineChunksTwoRoundCrsW1(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, true, true, kCoop, false, ShippedTune, 1>(a);
 }
 
 // The same held to at least kMinWaves waves per SIMD (a register bound:
@@ -1010,6 +1021,12 @@ template <class K, int kLoss, bool kCrs, class T = PointsOnlyTune>
 __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksFusedPoints(
     const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, kCrs, 2, true, T>(a);
+}
+// One wave per workgroup (A/B builds, CSE_FUSEDPOINTS_W1).
+template <class K, int kLoss, bool kCrs, class T = PointsOnlyTune>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+EvaluateAffineChunksFusedPointsW1(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, true, kCrs, 2, true, T, 1>(a);
 }
 
 // Slot-0 (camera) part of the fused gradient, by re-evaluation in camera

@@ -354,9 +354,9 @@ __global__ __launch_bounds__(kBlockThreads) void MultiplyTableKernel(const Group
 //   * slot 0 (cameras): F_b^T z_b in block order (GradientContribKernel and
 //     GradientChunkReduceKernel add them per camera, fixed order).
 // Deterministic; the host requires the fused gradient's eligibility.
-template <class K, bool kCrs>
-__global__ __launch_bounds__(kBlockThreads) void CgnrMultiplyKernel(const GroupArgs a,
-                                                                    const double* x, double* y) {
+template <class K, bool kCrs, int kWPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWPB * kWave) void CgnrMultiplyKernel(const GroupArgs a,
+                                                                   const double* x, double* y) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, N = Tr::N;
   static_assert(Tr::NB == 2 && NR == 2 && S1 == 3, "Snavely-shaped groups");
@@ -364,10 +364,10 @@ __global__ __launch_bounds__(kBlockThreads) void CgnrMultiplyKernel(const GroupA
   constexpr int kImg = kWave * NR * N;        // doubles of one wave's Jacobian image
   constexpr int kPieces = kImg / (2 * kWave);  // 16-byte DMA pieces per lane
   static_assert(kImg % (2 * kWave) == 0 && (kWave * NR * S0) % (2 * kWave) == 0, "16-B pieces");
-  __shared__ double img[kWavesPerBlock][kImg];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  __shared__ double img[kWPB][kImg];
+  const int lane = threadIdx.x & (kWave - 1), wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
   const int64_t nchunks = (a.n + kWave - 1) / kWave;
-  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
   if (c >= nchunks) return;
   double* im = img[wave];
   const int64_t i0 = c * kWave;

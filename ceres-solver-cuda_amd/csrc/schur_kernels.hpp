@@ -185,15 +185,16 @@ __device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, cons
 // pieces, up to 1 KiB per instruction), as CgnrMultiplyKernel's image; each
 // lane reads its block's cells from LDS.  The contributions F_b^T u_b are
 // staged through the same LDS and leave as contiguous 16-byte pieces.
-template <int S0, int kMode>
-__global__ __launch_bounds__(kBlockThreads) void SchurChunkKernel(const SchurArgs a) {
+// kWPB: waves per workgroup (chunk = workgroup * kWPB + wave).
+template <int S0, int kMode, int kWPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs a) {
   constexpr int S0p = (S0 + 1) & ~1;
   constexpr int kF = 2 * S0;                // doubles per F cell
   constexpr int kImg = kWave * (kF + 6);    // F cells, then E cells, of up to a wave of blocks
   static_assert(kF % 2 == 0 && kWave * S0p <= kImg, "16-byte pieces; contributions fit");
-  __shared__ double img_all[kWavesPerBlock][kImg];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  __shared__ double img_all[kWPB][kImg];
+  const int lane = threadIdx.x & (kWave - 1), wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
+  const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
   if (c >= a.nchunks) return;
   double* im = img_all[wave];
   const int64_t i0 = a.chunk_begin[2 * c];
