@@ -245,17 +245,19 @@ void LaunchTable(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 // The affine kernel: one 64-block chunk per wave, 4 waves per workgroup.
-// CSE_CHUNKS_W1 (A/B builds): the residual-only and cost-only forms with one
-// wave per workgroup.
-#ifndef CSE_CHUNKS_W1
-#define CSE_CHUNKS_W1 0
+// CSE_CHUNKS_WPB (A/B builds): the residual-only and cost-only forms with
+// this many waves per workgroup (one measured 1 % slower than four,
+// profiles/round3/w1).
+#ifndef CSE_CHUNKS_WPB
+#define CSE_CHUNKS_WPB 4
 #endif
 template <class K, int L, bool J, bool Crs, int Co, class T = cse::ShippedTune>
 void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  if constexpr (CSE_CHUNKS_W1 != 0 && !J) {
+  if constexpr (CSE_CHUNKS_WPB != cse::kWavesPerBlock && !J) {
+    constexpr int W = CSE_CHUNKS_WPB;
     const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-    hipLaunchKernelGGL((cse::EvaluateAffineChunksW1<K, L, J, Crs, Co, T>), dim3((unsigned)chunks),
-                       dim3(cse::kWave), 0, s, a);
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksW<K, L, J, Crs, Co, T, W>),
+                       dim3((unsigned)((chunks + W - 1) / W)), dim3(W * cse::kWave), 0, s, a);
   } else {
     hipLaunchKernelGGL((cse::EvaluateAffineChunks<K, L, J, Crs, Co, T>), dim3((unsigned)num_wg),
                        dim3(cse::kBlockThreads), 0, s, a);
@@ -270,7 +272,7 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 // the same for the fused-gradient points kernel (CSE_FUSEDPOINTS_W1),
 // gradient evaluation 2.147-2.153 -> 2.107-2.109 ms.  The residual-only
 // kernel (8 waves per SIMD) measured +1 % that way and keeps four
-// (CSE_CHUNKS_W1 0).
+// (CSE_CHUNKS_WPB 4).
 #ifndef CSE_TWOROUND_W1
 #define CSE_TWOROUND_W1 1
 #endif

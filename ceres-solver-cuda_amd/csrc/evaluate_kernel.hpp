@@ -957,10 +957,10 @@ template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T = Shipped
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const GroupArgs a) {
   AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T>(a);
 }
-// One wave per workgroup (A/B builds, CSE_CHUNKS_W1).
-template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T = ShippedTune>
-__global__ __launch_bounds__(kWave) void EvaluateAffineChunksW1(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T, 1>(a);
+// kWPB waves per workgroup (A/B builds, CSE_CHUNKS_WPB).
+template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T, int kWPB>
+__global__ __launch_bounds__(kWPB * kWave) void EvaluateAffineChunksW(const GroupArgs a) {
+  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T, kWPB>(a);
 }
 
 // The shipped BSM Jacobian kernel of two-slot kinds: two-round staging (36
