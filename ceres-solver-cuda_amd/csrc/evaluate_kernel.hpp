@@ -974,8 +974,11 @@ __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound
 // The same with one wave per workgroup (9 KiB of LDS each, 16 per CU): each
 // wave is dispatched and retired on its own, so the CU's waves do not start
 // and reach their store tails in groups of four.
+#ifndef CSE_W1_WAVES_PER_EU
+#define CSE_W1_WAVES_PER_EU 4
+#endif
 template <class K, int kLoss, int kCoop, class T = ShippedTune>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(CSE_W1_WAVES_PER_EU))) void
 EvaluateAffineChunksTwoRoundW1(const GroupArgs a) {
   static_assert(kTwoRoundBsm<K>, "two-slot kinds");
   AffineChunkBody<K, kLoss, true, false, kCoop, false, T, 1>(a);
