@@ -27,6 +27,9 @@ Besides the headline, the default line carries secondary legs measured in the
 same run (each with its own barrier-bracketed timing, max over ranks):
   gradient       residual+Jacobian+gradient J^T r (what the trust-region
                  minimizer requests, trust_region_minimizer.cc:242-255)
+  same_point     the headline evaluation with new_evaluation_point = false
+                 (CSE_EVAL_SAME_POINT: the Jacobian at a just-accepted
+                 candidate, trust_region_minimizer.cc:822-826; no repack)
   residual_only  residuals + cost (trust_region_minimizer.cc:770-788)
   host_strips    evaluation + D2H of each rank's residual and Jacobian
                  strips into pinned host memory (the reference's seam,
