@@ -1079,6 +1079,13 @@ int CamGradSortedInputs(Group& G, hipStream_t s) {
   return CSE_OK;
 }
 
+// Waves per workgroup of CameraGradientKernel (one chunk per wave either
+// way); CSE_CAMGRAD_W1 (A/B builds) launches it one wave per workgroup.
+#ifndef CSE_CAMGRAD_W1
+#define CSE_CAMGRAD_W1 0
+#endif
+constexpr int kCamGradWavesPerWg = CSE_CAMGRAD_W1 ? 1 : cse::kWavesPerBlock;
+
 // CameraGradientKernel: the per-chunk slot-0 sums into P.chunk_partial.
 int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hipStream_t s) {
   const Group::GradPlan& P = G.grad[0];
@@ -1101,22 +1108,23 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
     cg.packed_lo = G.slot0_lo;
     cg.packed_stride = G.packed_stride;
   }
-  const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
+  constexpr int W = kCamGradWavesPerWg;
+  const dim3 grid((unsigned)((P.nchunks + W - 1) / W));
   if (P.nchunks > 0) {
     auto launch = [&](auto kd) {
       using K = decltype(kd);
       switch (G.loss.kind) {
         case CSE_LOSS_HUBER:
-          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossHuber>), grid,
-                             dim3(cse::kBlockThreads), 0, s, cg);
+          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossHuber, W>), grid,
+                             dim3(W * cse::kWave), 0, s, cg);
           break;
         case CSE_LOSS_CAUCHY:
-          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossCauchy>), grid,
-                             dim3(cse::kBlockThreads), 0, s, cg);
+          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossCauchy, W>), grid,
+                             dim3(W * cse::kWave), 0, s, cg);
           break;
         default:
-          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossTrivial>), grid,
-                             dim3(cse::kBlockThreads), 0, s, cg);
+          hipLaunchKernelGGL((cse::CameraGradientKernel<K, cse::kLossTrivial, W>), grid,
+                             dim3(W * cse::kWave), 0, s, cg);
       }
     };
     if (G.kind == kKindQuaternionTangent) launch(cse::SnavelyQuaternionTangentKind{});

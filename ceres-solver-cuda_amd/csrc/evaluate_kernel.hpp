@@ -1095,14 +1095,14 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
   }
 }
 
-template <class K, int kLoss>
-__global__ __launch_bounds__(kBlockThreads) void CameraGradientKernel(const CamGradArgs g) {
+template <class K, int kLoss, int kWPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWPB * kWave) void CameraGradientKernel(const CamGradArgs g) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, D = Tr::D;
   static_assert(Tr::NB == 2 && S1 > 0, "two-slot kinds");
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int wave = kWPB == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t cid = (int64_t)blockIdx.x * kWPB + wave;
   if (cid >= g.nchunks) return;
   const int64_t q0 = g.chunk_begin[cid], q1 = g.chunk_begin[cid + 1];
   constexpr int X0 = Tr::X0;
