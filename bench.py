@@ -35,8 +35,9 @@ same run (each with its own barrier-bracketed timing, max over ranks):
                  strips into pinned host memory (the reference's seam,
                  README.md:198-200; PCIe-inclusive, never `value`)
 and, on rank 0 at N=1, the CPU baseline (the oracle, oracle/, built
--O3 -march=native on this host) at 1 thread and at the box's CPU share, for
-residual+Jacobian and residual-only.
+-O3 -march=native on this host) on every physical core of the affinity mask
+(the headline CPU leg, `speedup_vs_cpu`), at the box's CPU share and at 1
+thread, for residual+Jacobian and residual-only.
 
 Data is synthetic (no BAL file is available offline; see ceres_amd/bal.py for
 the generator), with the exact BAL header counts.  Rank 0 prints one JSON
@@ -102,7 +103,9 @@ def parse():
     ap.add_argument("--host-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = the box's CPU share ($OMP_NUM_THREADS, else the affinity mask)")
+                    help="threads of the CPU baseline's headline leg; 0 = one per physical core "
+                         "of the affinity mask (a leg at the box's CPU share, $OMP_NUM_THREADS, "
+                         "and a 1-thread leg are timed beside it)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
     ap.add_argument("--lib", default=None, help="load this build of libcse.so (A/B runs)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -143,24 +146,35 @@ def make_loss(name):
 # CPU baseline (rank 0, N = 1): the oracle restatement of ProgramEvaluator
 # ---------------------------------------------------------------------------
 def _host_info():
-    model, phys = None, set()
-    pid = None
+    """CPU model, sockets and physical cores of the host, and the physical
+    cores inside this process's affinity mask (the cores the all-core leg
+    may use: one thread per physical core, SMT siblings left idle, as the
+    reference's benchmark sweeps num_threads up to the core count,
+    evaluation_benchmark.cc:206-210)."""
+    model, phys, cpu_core = None, set(), {}
+    pid, proc = None, None
     try:
         with open("/proc/cpuinfo") as fh:
             for line in fh:
                 k, _, v = line.partition(":")
                 k, v = k.strip(), v.strip()
-                if k == "model name" and model is None:
+                if k == "processor":
+                    proc = int(v)
+                elif k == "model name" and model is None:
                     model = v
                 elif k == "physical id":
                     pid = v
                 elif k == "core id":
                     phys.add((pid, v))
+                    if proc is not None:
+                        cpu_core[proc] = (pid, v)
     except OSError:
         pass
+    aff = os.sched_getaffinity(0)
+    in_mask = {cpu_core[c] for c in aff if c in cpu_core}
     return {"cpu_model": model, "logical_cpus": os.cpu_count(),
             "sockets": len({p for p, _ in phys}) or None, "physical_cores": len(phys) or None,
-            "affinity_cpus": len(os.sched_getaffinity(0))}
+            "affinity_cpus": len(aff), "physical_cores_in_affinity": len(in_mask) or len(aff)}
 
 
 def _oracle_module():
@@ -179,11 +193,13 @@ def _oracle_module():
     return O, build
 
 
-def cpu_baseline(args, arrays, threads):
+def cpu_baseline(args, arrays, threads, share):
     """The oracle on bounded, point-bucket-aligned samples of the workload:
-    residual+Jacobian and residual-only, at `threads` and at 1 thread.
-    value = the multithreaded residual+Jacobian rate, in whole-workload
-    evaluations per second (blocks per second / the workload's blocks)."""
+    residual+Jacobian and residual-only at `threads` (one per physical core
+    of the affinity mask: the all-core leg, `value`), at `share` (the box's
+    CPU share, $OMP_NUM_THREADS) and at 1 thread.  value = the all-core
+    residual+Jacobian rate in whole-workload evaluations per second (blocks
+    per second / the workload's blocks)."""
     O, build = _oracle_module()
     cams, pts, ci, pi, obs = arrays
     total = len(ci)
@@ -202,10 +218,12 @@ def cpu_baseline(args, arrays, threads):
         return S, prog
 
     legs = {}
+    counts = sorted({threads, share, 1}, reverse=True)
     for jac in (True, False):
-        for nt in (threads, 1):
-            # about 1 s per timed evaluation: the whole workload multithreaded,
-            # a 1/16 (Jacobian) or 1/8 (residual-only) sample on one thread
+        for nt in counts:
+            # about 1 s per timed evaluation or less: the whole workload
+            # multithreaded, a 1/16 (Jacobian) or 1/8 (residual-only) sample on
+            # one thread
             S, prog = sample(total if nt > 1 else total // (16 if jac else 8))
             ev = O.OracleProgram.from_program(prog).evaluator(nt)
             r = np.empty(prog.num_residuals)
@@ -226,9 +244,11 @@ def cpu_baseline(args, arrays, threads):
     head = legs[f"jacobian_{threads}t"]
     return {"value": head["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
             "sample": (f"residual+Jacobian of all {total:,} residual blocks of the same workload "
-                       f"on {threads} threads, median of 3 after a warm-up; legs: 1-thread runs "
-                       f"on the first 1/16 (Jacobian) or 1/8 (residual-only) of the blocks, cut "
-                       f"at a point bucket; value = blocks/s / {total:,}"),
+                       f"on {threads} threads (one per physical core of the affinity mask), "
+                       f"median of 3 after a warm-up; legs: the same at the box's CPU share "
+                       f"({share} threads), and 1-thread runs on the first 1/16 (Jacobian) or "
+                       f"1/8 (residual-only) of the blocks, cut at a point bucket; value = "
+                       f"blocks/s / {total:,}"),
             "build": build, "host": _host_info(), "legs": legs}
 
 
@@ -469,18 +489,27 @@ def main():
             devices = list(range(ndev))
             mev = ca.Evaluator(prog, devices=devices, profile=True)
             bufs = (np.empty(prog.num_residuals), None, np.empty(prog.num_jacobian_values))
+            hstate = np.array(prog.state)
+            pinned = [hstate, bufs[0], bufs[2]]
+            for a in pinned:  # page-locked by the caller (cse_host_register)
+                ca.host_register(a)
             hs = max(2, args.host_steps)
-            mev.evaluate(residuals=True, gradient=False, jacobian=True, out=bufs)  # registers
+            mev.evaluate(hstate, residuals=True, gradient=False, jacobian=True, out=bufs)
             t0 = time.perf_counter()
             for _ in range(hs):
-                ok = mev.evaluate(residuals=True, gradient=False, jacobian=True, out=bufs)[0]
+                ok = mev.evaluate(hstate, residuals=True, gradient=False, jacobian=True, out=bufs)[0]
                 assert ok
             e = time.perf_counter() - t0
             first, _ = mev.shard_info()
+            h2d, d2h = mev.transfer_bytes()
             mev.close()
+            for a in pinned:
+                ca.host_unregister(a)
             secondary["host_multi"] = {
                 "value": hs / e, "unit": "evals/s", "ms_per_step": e / hs * 1e3, "steps": hs,
                 "devices": devices, "shard_first_blocks": [int(x) for x in first],
+                "state_h2d_bytes_per_shard": [int(x) for x in h2d],
+                "strips_d2h_bytes_per_shard": [int(x) for x in d2h],
                 "d2h_bytes": 8 * (prog.num_residuals + prog.num_jacobian_values),
                 "d2h_GBps": 8 * (prog.num_residuals + prog.num_jacobian_values) * hs / e / 1e9,
                 "what": "cse_evaluate on a cse_create_multi evaluator over every visible device "
@@ -492,10 +521,11 @@ def main():
     if rank == 0:
         cpu = None
         if arrays is not None:
-            share = len(os.sched_getaffinity(0))
+            aff = len(os.sched_getaffinity(0))
             omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-            threads = args.cpu_threads or (min(omp, share) if omp > 0 else share)
-            cpu = cpu_baseline(args, arrays, threads)
+            share = min(omp, aff) if omp > 0 else aff
+            threads = args.cpu_threads or _host_info()["physical_cores_in_affinity"]
+            cpu = cpu_baseline(args, arrays, threads, share)
         traffic = None
         pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}_{args.loss}_{args.format}.json")
         if (world == 1 and args.mode == "jacobian" and not args.gradient and not variant
@@ -568,6 +598,13 @@ def main():
             },
             "secondary": secondary,
             "schur_init_ms": schur_init_ms if args.mode == "schur" else None,
+            "parity": ("outputs checked against the oracle (Ceres' CPU ProgramEvaluator restated, "
+                       "oracle/) by tests/ at Eigen isApprox 1e-13 per vector "
+                       "(evaluator_cuda_test.cu.cc:61) plus 1e-10 per element, except the Jacobian "
+                       "cells and gradient rows of cameras with 0 < theta < 1e-3 (series Rodrigues "
+                       "form), held to 1e-7 against the reference form and 1e-13 against 40-digit "
+                       "values (DESIGN.md section 6 item 5); the synthetic workload has no such "
+                       "camera"),
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / world / cpu["value"]) if cpu else None,
             "build_s": build_s,

@@ -10,9 +10,9 @@ from ._cse import (LOSS_CAUCHY, LOSS_HUBER, LOSS_TRIVIAL, POINT_DISPLACEMENT_3_3
                    SNAVELY_2_9_3, SNAVELY_NO_DISTORTION_2_7_3, SNAVELY_QUATERNION_2_10_3,
                    FUNCTOR_SHAPES)
 from .problem import (BLOCK_SPARSE, COMPRESSED_ROW, Evaluator, Loss, Program, ProblemCUDA,
-                      ResidualGroup)
+                      ResidualGroup, host_register, host_unregister)
 
 __all__ = ["bal", "Evaluator", "Loss", "Program", "ProblemCUDA", "ResidualGroup",
            "BLOCK_SPARSE", "COMPRESSED_ROW", "SNAVELY_2_9_3", "SNAVELY_NO_DISTORTION_2_7_3",
            "SNAVELY_QUATERNION_2_10_3", "POINT_DISPLACEMENT_3_3", "LOSS_TRIVIAL", "LOSS_HUBER",
-           "LOSS_CAUCHY", "FUNCTOR_SHAPES"]
+           "LOSS_CAUCHY", "FUNCTOR_SHAPES", "host_register", "host_unregister"]

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libcse.so"))
 
-CSE_ABI_VERSION = 1
+CSE_ABI_VERSION = 2
 CSE_OK = 0
 CSE_EVALUATION_FAILED = 1
 CSE_ERR_INVALID = -1
@@ -154,6 +154,9 @@ SIGNATURES = {
     "cse_create_multi": (C.c_int, [C.POINTER(cse_problem_desc), C.POINTER(cse_options),
                                    P_i32, C.c_int32, C.POINTER(C.c_void_p)]),
     "cse_shard_info": (C.c_int, [C.c_void_p, P_i32, P_i64, P_i32]),
+    "cse_shard_transfer_bytes": (C.c_int, [C.c_void_p, P_i64, P_i64]),
+    "cse_host_register": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "cse_host_unregister": (C.c_int, [C.c_void_p]),
     "cse_destroy": (None, [C.c_void_p]),
     "cse_last_error": (C.c_char_p, []),
     "cse_get_info": (C.c_int, [C.c_void_p, C.POINTER(cse_info)]),

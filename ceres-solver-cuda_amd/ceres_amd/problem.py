@@ -408,6 +408,22 @@ class ProblemCUDA:
         return prog
 
 
+def host_register(arr):
+    """Page-lock a C-contiguous numpy array for asynchronous transfers
+    (cse_host_register) until host_unregister(arr); the multi-device
+    evaluator copies into and out of such buffers without staging.  Keep the
+    array alive while registered."""
+    arr = np.asarray(arr)
+    if not arr.flags.c_contiguous or arr.nbytes == 0:
+        raise ValueError("host_register: a non-empty C-contiguous array")
+    _cse.check(_cse.lib().cse_host_register(arr.ctypes.data, arr.nbytes), "cse_host_register")
+    return arr
+
+
+def host_unregister(arr):
+    _cse.check(_cse.lib().cse_host_unregister(np.asarray(arr).ctypes.data), "cse_host_unregister")
+
+
 class Evaluator:
     """ProgramEvaluatorCUDA seam over libcse.so (program_evaluator_cuda.h:65-183)."""
 
@@ -471,6 +487,18 @@ class Evaluator:
         _cse.check(L.cse_shard_info(self.handle, C.byref(n), _ptr(first, C.c_int64),
                                     _ptr(devs, C.c_int32)), "cse_shard_info")
         return first, devs
+
+    def transfer_bytes(self):
+        """Per shard: (state bytes copied to its device, strip bytes copied
+        back) by one host-pointer evaluate (cse_shard_transfer_bytes)."""
+        first, _ = self.shard_info()
+        n = len(first) - 1
+        h2d = np.empty(n, np.int64)
+        d2h = np.empty(n, np.int64)
+        _cse.check(_cse.lib().cse_shard_transfer_bytes(self.handle, _ptr(h2d, C.c_int64),
+                                                        _ptr(d2h, C.c_int64)),
+                   "cse_shard_transfer_bytes")
+        return h2d, d2h
 
     def evaluate(self, state=None, residuals=True, gradient=True, jacobian=True, out=None,
                  new_evaluation_point=True):

@@ -182,6 +182,10 @@ struct Group {
   int64_t slot0_count = 0;
   int slot0_stride = 0;
   int packed_stride = 0;  // row stride of the repacked slot-0 table (doubles)
+  // The manifold DetectAffine chose for slot 0, taken from the first block
+  // with an active slot 0 (held blocks carry no Jacobian columns, so their
+  // own manifold does not matter).
+  int slot0_manifold = CSE_MANIFOLD_MATRIX;
   DevBuf<double> packed0;
   // Gradient post-pass plan per slot (affine groups with a Jacobian layout).
   struct GradPlan {
@@ -846,6 +850,7 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
     manifold[0] = CSE_MANIFOLD_QUATERNION_EUCLIDEAN;
     sizes[0] = k.s0 - 1;
   }
+  G->slot0_manifold = manifold[0];
   // Constant slot-0 blocks (a held camera) are allowed for the kinds with the
   // constant-aware kernels (the 9-column cameras, cse::ShippedTuneC0).
   const bool const0_ok = k.nb == 2 && (g.functor_kind == CSE_FUNCTOR_SNAVELY_2_9_3 ||
@@ -1565,9 +1570,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     G.affine = G.policy != kTable;
     if (!G.affine) G.const0 = false;  // DetectAffine may have set it before giving up
     if (G.affine && g.functor_kind == CSE_FUNCTOR_SNAVELY_QUATERNION_2_10_3 &&
-        d->parameter_blocks[g.parameter_block_ids[0]].manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
-      // Slot 0 on the quaternion manifold (DetectAffine checked every
-      // block): the kernel kind with the tangent Jacobian (k follows G.shape).
+        G.slot0_manifold == CSE_MANIFOLD_QUATERNION_EUCLIDEAN) {
+      // Slot 0 on the quaternion manifold (DetectAffine checked every active
+      // block; a held camera's own manifold is irrelevant): the kernel kind
+      // with the tangent Jacobian (k follows G.shape).
       G.kind = kKindQuaternionTangent;
       ShapeOf(G.kind, &G.shape);
     }
@@ -2242,6 +2248,19 @@ int cse_shard_info(cse_evaluator* ev, int32_t* num_shards, int64_t* first_block,
   if (devices) devices[0] = ev->device;
   return CSE_OK;
 }
+
+int cse_shard_transfer_bytes(cse_evaluator* ev, int64_t* state_h2d_bytes, int64_t* strips_d2h_bytes) {
+  if (!ev) return Fail(CSE_ERR_INVALID, "null evaluator");
+  if (ev->multi) return MultiTransferBytes(ev->multi, state_h2d_bytes, strips_d2h_bytes);
+  if (state_h2d_bytes) state_h2d_bytes[0] = ev->num_parameters * (int64_t)sizeof(double);
+  if (strips_d2h_bytes)
+    strips_d2h_bytes[0] = (ev->num_residuals + ev->num_jacobian_values) * (int64_t)sizeof(double);
+  return CSE_OK;
+}
+
+int cse_host_register(void* p, size_t bytes) { return CseHostRegister(p, bytes); }
+
+int cse_host_unregister(void* p) { return CseHostUnregister(p); }
 
 int cse_get_info(cse_evaluator* ev, cse_info* info) {
   if (!ev || !info) return Fail(CSE_ERR_INVALID, "null argument");

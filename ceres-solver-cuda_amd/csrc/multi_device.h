@@ -9,11 +9,12 @@
 // boundaries, gives each shard an ordinary evaluator on its
 // device, and on each Evaluate copies every shard's residual and Jacobian
 // strips straight into disjoint regions of the caller's one residual and
-// values buffers (page-locked once), while the cost and the gradient rows
+// values buffers (asynchronously when the caller page-locked them), while the cost and the gradient rows
 // are summed over the shards in a fixed order on the host.
 #ifndef CSE_MULTI_DEVICE_H_
 #define CSE_MULTI_DEVICE_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include <string>
@@ -37,6 +38,9 @@ int MultiInfo(CseMulti* m, cse_info* info);
 int MultiShardInfo(CseMulti* m, int32_t* num_shards, int64_t* first_block, int32_t* devices);
 int MultiSetPlusJacobians(CseMulti* m, const double* plus_jacobians);
 int MultiPlus(CseMulti* m, const double* state, const double* delta, double* state_plus_delta);
+int MultiTransferBytes(CseMulti* m, int64_t* state_h2d, int64_t* strips_d2h);
+int CseHostRegister(void* p, size_t bytes);
+int CseHostUnregister(void* p);
 int MultiKernelStats(CseMulti* m, double* last_ms, double* total_ms, int64_t* launches);
 int MultiResetKernelStats(CseMulti* m);
 

@@ -14,18 +14,31 @@
 // them -- the bucket cuts only keep each point's rows in one shard.
 //
 // Each shard becomes an ordinary evaluator (cse_create) of a sub-descriptor:
-// the shard's blocks renumbered from 0, every parameter block, and the
-// residual / Jacobian-value offsets of its blocks mapped onto a compact local
-// range.  The local ranges are the union of the offsets the shard's blocks
-// write, kept as a list of global intervals (a Schur-ordered BlockSparse
-// shard: two, its E strip and its F strip; CompressedRow: one), so one
-// Evaluate hands every interval back with one D2H copy into the caller's
-// buffer at the interval's global position.  Cost and gradient: per shard on
-// its device, then summed over the shards in shard order (deterministic).
+// the shard's blocks renumbered from 0, only the parameter blocks they use
+// (renumbered in id order: every camera the shard sees plus its own points,
+// SURVEY.md §8(e)), and the state, delta, residual and Jacobian-value offsets
+// of those mapped onto compact local ranges.  Each local range is the union of
+// the global offsets involved, kept as a list of global intervals (a
+// Schur-ordered BlockSparse shard: its point slice and its cameras for the
+// state, its E strip and its F strip for the values; CompressedRow: one), so
+// one Evaluate moves every interval with one copy at its global position: the
+// state slices host-to-device, the strips device-to-host.  Renumbering in id
+// order and compacting in offset order keep an affine layout affine (a
+// shard's points and cameras stay on the fast kernels).  Cost and gradient:
+// per shard on its device, then summed over the shards in shard order
+// (deterministic).  Parameter blocks no residual block uses go to shard 0, so
+// Plus covers every active block.
+//
+// Host buffers.  Asynchronous copies need page-locked memory.  The caller
+// pins a buffer explicitly (cse_host_register, or its own hipHostMalloc);
+// the library never pins or caches a caller buffer by address (a freed
+// buffer's address can be reused by the next allocation).  A buffer that is
+// not pinned is copied synchronously.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -110,11 +123,16 @@ struct CseMulti {
     cse_evaluator* ev = nullptr;
     hipStream_t stream = nullptr;
     int64_t g0 = 0, g1 = 0;
-    std::vector<Interval> res_iv, jac_iv, grad_iv;
-    int64_t nres = 0, njac = 0, ngrad = 0;
+    // Global -> local intervals: state (active parameter blocks the shard
+    // uses), delta (their tangent columns: the gradient rows), residuals and
+    // Jacobian values (the strips).
+    std::vector<Interval> state_iv, res_iv, jac_iv, grad_iv;
+    int64_t nstate = 0, nres = 0, njac = 0, ngrad = 0;
     double *d_state = nullptr, *d_cost = nullptr, *d_res = nullptr, *d_jac = nullptr,
            *d_grad = nullptr;
     double *h_cost = nullptr, *h_grad = nullptr;  // pinned
+    // Plus staging (pinned, allocated on first use): local state, delta, result.
+    double *h_x = nullptr, *h_d = nullptr, *h_o = nullptr;
   };
   std::vector<Shard> shards;
   int64_t num_parameters = 0, num_effective = 0, num_residuals = 0, num_jacobian_values = 0;
@@ -123,12 +141,6 @@ struct CseMulti {
   // Every shard's d_state holds the state of the last evaluation queued
   // without error (CSE_EVAL_SAME_POINT skips the copies).
   bool state_current = false;
-  // The caller's host buffers, page-locked on first use (one per role).
-  struct Reg {
-    void* p = nullptr;
-    size_t bytes = 0;
-    bool ok = false;
-  } reg[3];  // state, residuals, Jacobian values
 };
 
 namespace {
@@ -139,33 +151,39 @@ void ReleaseShard(CseMulti::Shard& s) {
   (void)hipSetDevice(s.device);
   for (double* p : {s.d_state, s.d_cost, s.d_res, s.d_jac, s.d_grad})
     if (p) (void)hipFree(p);
-  for (double* p : {s.h_cost, s.h_grad})
+  for (double* p : {s.h_cost, s.h_grad, s.h_x, s.h_d, s.h_o})
     if (p) (void)hipHostFree(p);
   if (s.stream) (void)hipStreamDestroy(s.stream);
   s = CseMulti::Shard{};
 }
 
-// Page-locks the caller's buffer for role k (once per buffer; a new buffer
-// replaces the previous registration of that role).  Returns whether async
-// copies may use it; if registration fails the copies fall back to
-// synchronous pageable ones.
-bool Register(CseMulti* m, int k, const void* p, size_t bytes) {
-  auto& r = m->reg[k];
-  if (r.p == p && r.bytes == bytes) return r.ok;
-  if (r.p && r.ok) (void)hipHostUnregister(r.p);
-  r.p = const_cast<void*>(p);
-  r.bytes = bytes;
-  const hipError_t e = hipHostRegister(r.p, bytes, hipHostRegisterPortable);
-  if (e == hipErrorHostMemoryAlreadyRegistered) {
+// Ranges page-locked through cse_host_register (library-wide).
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [begin, end)
+
+// Is host memory at p page-locked by the HIP runtime (hipHostMalloc or
+// hipHostRegister, the caller's own)?
+bool RuntimePinned(const void* p) {
+  hipPointerAttribute_t at;
+  const hipError_t e = hipPointerGetAttributes(&at, p);
+  if (e != hipSuccess) {
     (void)hipGetLastError();
-    r.ok = true;  // already pinned by the caller (hipHostMalloc): keep, never unregister
-    r.p = nullptr;
-    r.bytes = 0;
-    return true;
+    return false;
   }
-  r.ok = e == hipSuccess;
-  if (!r.ok) (void)hipGetLastError();
-  return r.ok;
+  return at.type == hipMemoryTypeHost;
+}
+
+// May [p, p + bytes) take asynchronous copies?  Inside one cse_host_register
+// range, or pinned by the caller at both ends.
+bool Pinned(const void* p, size_t bytes) {
+  if (!p || bytes == 0) return false;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p), e = b + bytes;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (const auto& r : g_reg)
+      if (b >= r.first && e <= r.second) return true;
+  }
+  return RuntimePinned(p) && RuntimePinned(static_cast<const char*>(p) + bytes - 1);
 }
 
 // Cut positions in the global residual-block index (module comment).
@@ -189,12 +207,46 @@ std::vector<int64_t> BucketCuts(const std::vector<int64_t>& key, int n) {
   return cuts;
 }
 
-// The sub-descriptor of shard [g0, g1) and its evaluator.
+// Sorted, merged intervals of [begin, end) ranges given in any order.
+int64_t IntervalsOf(std::vector<std::pair<int64_t, int64_t>>& ranges, std::vector<Interval>* out) {
+  std::sort(ranges.begin(), ranges.end());
+  IntervalBuilder ib;
+  for (const auto& r : ranges) ib.Add(r.first, r.second);
+  return ib.Finish(out);
+}
+
+// The sub-descriptor of shard [g0, g1) and its evaluator.  used: the
+// parameter blocks the shard's residual blocks use (shard 0 also gets the
+// blocks no residual block uses).
 int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Shard& s,
-                const std::vector<Shape>& shapes) {
+                const std::vector<Shape>& shapes, const std::vector<char>& used) {
   const int64_t g0 = s.g0, g1 = s.g1, nloc = g1 - g0;
   const bool has_layout = d->jacobian_per_residual_layout && d->jacobian_per_residual_offsets;
-  // Groups restricted to the shard, renumbered from g0.
+  // Shard-local parameter blocks: the used ones, renumbered in id order; the
+  // active ones' state and delta ranges compacted in offset order.
+  std::vector<int32_t> lid(d->num_parameter_blocks, -1);
+  std::vector<cse_parameter_block> pbs;
+  {
+    std::vector<std::pair<int64_t, int64_t>> st, dl;
+    for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
+      if (!used[b]) continue;
+      lid[b] = (int32_t)pbs.size();
+      const cse_parameter_block& pb = d->parameter_blocks[b];
+      pbs.push_back(pb);
+      if (pb.is_constant) continue;
+      st.push_back({pb.state_offset, pb.state_offset + pb.size});
+      if (pb.tangent_size > 0) dl.push_back({pb.delta_offset, pb.delta_offset + pb.tangent_size});
+    }
+    s.nstate = IntervalsOf(st, &s.state_iv);
+    s.ngrad = IntervalsOf(dl, &s.grad_iv);
+    for (auto& pb : pbs) {
+      if (pb.is_constant) continue;  // offsets into the (whole) constant state
+      pb.state_offset = LocalOf(s.state_iv, pb.state_offset);
+      if (pb.tangent_size > 0) pb.delta_offset = LocalOf(s.grad_iv, pb.delta_offset);
+    }
+  }
+  // Groups restricted to the shard, renumbered from g0, ids mapped to the
+  // shard's parameter blocks.
   std::vector<cse_residual_group> groups;
   std::vector<std::vector<int64_t>> idx_store;
   std::vector<std::vector<int32_t>> ids_store;
@@ -207,12 +259,15 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
     const Shape& k = shapes[gi];
     const int ds = k.data;
     cse_residual_group sg = g;
+    ids_store.emplace_back();
+    auto& id = ids_store.back();
     if (!g.residual_block_index) {
       const int64_t lo = std::clamp<int64_t>(g0 - g.first_residual_block, 0, g.num_blocks);
       const int64_t hi = std::clamp<int64_t>(g1 - g.first_residual_block, 0, g.num_blocks);
       sg.num_blocks = hi - lo;
       sg.first_residual_block = g.first_residual_block + lo - g0;
-      sg.parameter_block_ids = g.parameter_block_ids ? g.parameter_block_ids + (int64_t)k.nb * lo : nullptr;
+      id.resize((size_t)((hi - lo) * k.nb));
+      for (int64_t q = 0; q < (hi - lo) * k.nb; ++q) id[q] = lid[g.parameter_block_ids[k.nb * lo + q]];
       sg.functor_data = g.functor_data ? g.functor_data + (int64_t)ds * lo : nullptr;
       for (int64_t i = lo; i < hi; ++i) {
         gr_of[g.first_residual_block + i - g0] = gi;
@@ -220,17 +275,14 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
       }
     } else {
       idx_store.emplace_back();
-      ids_store.emplace_back();
       data_store.emplace_back();
       auto& ix = idx_store.back();
-      auto& id = ids_store.back();
       auto& dt = data_store.back();
       for (int64_t i = 0; i < g.num_blocks; ++i) {
         const int64_t gg = g.residual_block_index[i];
         if (gg < g0 || gg >= g1) continue;
         ix.push_back(gg - g0);
-        id.insert(id.end(), g.parameter_block_ids + (int64_t)k.nb * i,
-                  g.parameter_block_ids + (int64_t)k.nb * (i + 1));
+        for (int j = 0; j < k.nb; ++j) id.push_back(lid[g.parameter_block_ids[(int64_t)k.nb * i + j]]);
         dt.insert(dt.end(), g.functor_data + (int64_t)ds * i, g.functor_data + (int64_t)ds * (i + 1));
         gr_of[gg - g0] = gi;
         i_of[gg - g0] = i;
@@ -238,14 +290,13 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
       sg.num_blocks = (int64_t)ix.size();
       sg.residual_block_index = ix.data();
       sg.first_residual_block = 0;
-      sg.parameter_block_ids = id.data();
       sg.functor_data = dt.data();
     }
+    sg.parameter_block_ids = id.data();
     groups.push_back(sg);
   }
-  // Residual, Jacobian-value and gradient intervals of the shard.
+  // Residual and Jacobian-value intervals of the shard.
   IntervalBuilder rb, jb;
-  std::vector<char> used(d->num_parameter_blocks, 0);
   for (int64_t l = 0; l < nloc; ++l) {
     const int gi = gr_of[l];
     if (gi < 0) continue;
@@ -260,10 +311,7 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
     int a = 0;
     for (int j = 0; j < k.nb; ++j) {
       const int32_t pid = g.parameter_block_ids[(int64_t)k.nb * i_of[l] + j];
-      if (pid < 0 || pid >= d->num_parameter_blocks)
-        return CseFail(CSE_ERR_INVALID, "parameter block id out of range");
       const cse_parameter_block& pb = d->parameter_blocks[pid];
-      used[pid] = 1;
       if (pb.is_constant || !has_layout) continue;
       const int64_t base = d->jacobian_per_residual_layout[gg] + (int64_t)a * k.nr;
       if (base < 0 || base + k.nr > d->num_jacobian_per_residual_offsets)
@@ -279,18 +327,6 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
   }
   s.nres = rb.Finish(&s.res_iv);
   s.njac = jb.Finish(&s.jac_iv);
-  {
-    std::vector<std::pair<int64_t, int64_t>> gs;
-    for (int64_t b = 0; b < d->num_parameter_blocks; ++b) {
-      const cse_parameter_block& pb = d->parameter_blocks[b];
-      if (used[b] && !pb.is_constant && pb.tangent_size > 0)
-        gs.push_back({pb.delta_offset, pb.delta_offset + pb.tangent_size});
-    }
-    IntervalBuilder gb;
-    std::sort(gs.begin(), gs.end());
-    for (const auto& r : gs) gb.Add(r.first, r.second);
-    s.ngrad = gb.Finish(&s.grad_iv);
-  }
   // Local layouts.
   std::vector<int64_t> res_layout(std::max<int64_t>(nloc, 1), 0), jac_layout, jac_offsets;
   if (has_layout) jac_layout.assign(std::max<int64_t>(nloc, 1), 0);
@@ -316,6 +352,10 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
   cse_problem_desc sd = *d;
   sd.num_groups = (int32_t)groups.size();
   sd.groups = groups.data();
+  sd.num_parameter_blocks = (int64_t)pbs.size();
+  sd.parameter_blocks = pbs.data();
+  sd.num_parameters = s.nstate;
+  sd.num_effective_parameters = s.ngrad;
   sd.num_residual_blocks = nloc;
   sd.num_residuals = s.nres;
   sd.residual_layout = res_layout.data();
@@ -337,9 +377,9 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
   auto dalloc = [&](double** p, int64_t n) -> hipError_t {
     return hipMalloc(reinterpret_cast<void**>(p), std::max<int64_t>(n, 1) * sizeof(double));
   };
-  if (dalloc(&s.d_state, d->num_parameters) != hipSuccess || dalloc(&s.d_cost, 1) != hipSuccess ||
+  if (dalloc(&s.d_state, s.nstate) != hipSuccess || dalloc(&s.d_cost, 1) != hipSuccess ||
       dalloc(&s.d_res, s.nres) != hipSuccess || dalloc(&s.d_jac, has_layout ? s.njac : 0) != hipSuccess ||
-      dalloc(&s.d_grad, d->num_effective_parameters) != hipSuccess)
+      dalloc(&s.d_grad, s.ngrad) != hipSuccess)
     return CseFail(CSE_ERR_OOM, "multi-device: device allocation failed on device " +
                                     std::to_string(s.device));
   MD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_cost), sizeof(double)));
@@ -394,12 +434,38 @@ int MultiCreate(const cse_problem_desc* d, const cse_options* options, const int
   const std::vector<int64_t> cuts = BucketCuts(key, n);
   key.clear();
   key.shrink_to_fit();
+  // Parameter blocks used by each shard (checked ids); shard 0 also takes
+  // the blocks no residual block uses.
+  std::vector<std::vector<char>> used(n, std::vector<char>(d->num_parameter_blocks, 0));
+  std::vector<char> any(d->num_parameter_blocks, 0);
+  for (int gi = 0; gi < d->num_groups; ++gi) {
+    const cse_residual_group& g = d->groups[gi];
+    const int nb = shapes[gi].nb;
+    for (int64_t i = 0; i < g.num_blocks; ++i) {
+      const int64_t gg = g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
+      const int k = (int)(std::upper_bound(cuts.begin(), cuts.end(), gg) - cuts.begin()) - 1;
+      for (int j = 0; j < nb; ++j) {
+        const int32_t pid = g.parameter_block_ids[(int64_t)nb * i + j];
+        if (pid < 0 || pid >= d->num_parameter_blocks) {
+          delete m;
+          return CseFail(CSE_ERR_INVALID, "parameter block id out of range");
+        }
+        used[k][pid] = 1;
+        any[pid] = 1;
+      }
+    }
+  }
+  for (int64_t b = 0; b < d->num_parameter_blocks; ++b)
+    if (!any[b]) used[0][b] = 1;
+  any.clear();
+  any.shrink_to_fit();
   m->shards.resize(n);
   for (int k = 0; k < n; ++k) {
     m->shards[k].device = devices[k];
     m->shards[k].g0 = cuts[k];
     m->shards[k].g1 = cuts[k + 1];
-    const int rc = CreateShard(d, &opts, m->shards[k], shapes);
+    const int rc = CreateShard(d, &opts, m->shards[k], shapes, used[k]);
+    std::vector<char>().swap(used[k]);
     if (rc) {
       MultiDestroy(m);
       return rc;
@@ -412,67 +478,105 @@ int MultiCreate(const cse_problem_desc* d, const cse_options* options, const int
 void MultiDestroy(CseMulti* m) {
   if (!m) return;
   for (auto& s : m->shards) ReleaseShard(s);
-  for (auto& r : m->reg)
-    if (r.p && r.ok) (void)hipHostUnregister(r.p);
   delete m;
 }
+
+namespace {
+
+// Synchronises the streams of shards [0, upto): the copies queued on them
+// read or write the caller's buffers, which must not be returned to the
+// caller (and freed) while in flight.
+void Drain(CseMulti* m, size_t upto) {
+  for (size_t k = 0; k < upto && k < m->shards.size(); ++k) {
+    auto& s = m->shards[k];
+    if (!s.stream) continue;
+    (void)hipSetDevice(s.device);
+    (void)hipStreamSynchronize(s.stream);
+  }
+}
+
+}  // namespace
 
 int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residuals,
                   double* gradient, double* jac, bool same_point) {
   if (jac && !m->has_layout)
     return CseFail(CSE_ERR_INVALID, "Jacobian requested but the descriptor had no Jacobian layout");
-  const bool async_state = Register(m, 0, state, m->num_parameters * sizeof(double));
-  const bool async_res = residuals && Register(m, 1, residuals, m->num_residuals * sizeof(double));
-  const bool async_jac = jac && Register(m, 2, jac, m->num_jacobian_values * sizeof(double));
-  // Queue every shard: state H2D, evaluation, strips D2H (disjoint regions of
-  // the caller's buffers), gradient rows and cost into pinned staging.
+  const bool async_state = Pinned(state, m->num_parameters * sizeof(double));
+  const bool async_res = residuals && Pinned(residuals, m->num_residuals * sizeof(double));
+  const bool async_jac = jac && Pinned(jac, m->num_jacobian_values * sizeof(double));
+  // Queue every shard: its state slices H2D, evaluation, strips D2H (disjoint
+  // regions of the caller's buffers), gradient rows and cost into pinned
+  // staging.  Any error drains the shards queued so far before returning.
   const bool copy_state = !(same_point && m->state_current);
   m->state_current = false;
+  size_t queued = 0;
+#define MD_Q(call)                                                                         do {                                                                                       hipError_t e_ = (call);                                                                  if (e_ != hipSuccess) {                                                                    Drain(m, queued + 1);                                                                    return CseFail(CSE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));        }                                                                                      } while (0)
   for (auto& s : m->shards) {
-    MD_HIP(hipSetDevice(s.device));
-    if (m->num_parameters > 0 && copy_state) {
-      if (async_state)
-        MD_HIP(hipMemcpyAsync(s.d_state, state, m->num_parameters * sizeof(double),
-                              hipMemcpyHostToDevice, s.stream));
-      else
-        MD_HIP(hipMemcpy(s.d_state, state, m->num_parameters * sizeof(double), hipMemcpyHostToDevice));
-    }
+    MD_Q(hipSetDevice(s.device));
+    if (copy_state)
+      for (const auto& iv : s.state_iv) {
+        const size_t bytes = (iv.end - iv.begin) * sizeof(double);
+        if (async_state)
+          MD_Q(hipMemcpyAsync(s.d_state + iv.local, state + iv.begin, bytes, hipMemcpyHostToDevice,
+                              s.stream));
+        else
+          MD_Q(hipMemcpy(s.d_state + iv.local, state + iv.begin, bytes, hipMemcpyHostToDevice));
+      }
     int rc = cse_evaluate_device_ex(s.ev, s.d_state, s.d_cost, residuals ? s.d_res : nullptr,
                                     gradient ? s.d_grad : nullptr, jac ? s.d_jac : nullptr,
                                     same_point ? CSE_EVAL_SAME_POINT : 0u);
-    if (rc) return rc;
-    MD_HIP(hipMemcpyAsync(s.h_cost, s.d_cost, sizeof(double), hipMemcpyDeviceToHost, s.stream));
+    if (rc) {
+      Drain(m, queued + 1);
+      return rc;
+    }
+    MD_Q(hipMemcpyAsync(s.h_cost, s.d_cost, sizeof(double), hipMemcpyDeviceToHost, s.stream));
     if (residuals && async_res)
       for (const auto& iv : s.res_iv)
-        MD_HIP(hipMemcpyAsync(residuals + iv.begin, s.d_res + iv.local,
-                              (iv.end - iv.begin) * sizeof(double), hipMemcpyDeviceToHost, s.stream));
+        MD_Q(hipMemcpyAsync(residuals + iv.begin, s.d_res + iv.local,
+                            (iv.end - iv.begin) * sizeof(double), hipMemcpyDeviceToHost, s.stream));
     if (jac && async_jac)
       for (const auto& iv : s.jac_iv)
-        MD_HIP(hipMemcpyAsync(jac + iv.begin, s.d_jac + iv.local, (iv.end - iv.begin) * sizeof(double),
-                              hipMemcpyDeviceToHost, s.stream));
-    if (gradient)
-      for (const auto& iv : s.grad_iv)
-        MD_HIP(hipMemcpyAsync(s.h_grad + iv.local, s.d_grad + iv.begin,
-                              (iv.end - iv.begin) * sizeof(double), hipMemcpyDeviceToHost, s.stream));
+        MD_Q(hipMemcpyAsync(jac + iv.begin, s.d_jac + iv.local, (iv.end - iv.begin) * sizeof(double),
+                            hipMemcpyDeviceToHost, s.stream));
+    if (gradient && s.ngrad > 0)
+      MD_Q(hipMemcpyAsync(s.h_grad, s.d_grad, s.ngrad * sizeof(double), hipMemcpyDeviceToHost,
+                          s.stream));
+    ++queued;
   }
   m->state_current = true;
   // Wait for every shard (cse_wait synchronises the shard's stream, which
-  // carries the copies too) and collect the statuses.
-  int status = CSE_OK;
+  // carries the copies too) and collect the statuses; every shard is waited
+  // for even after an error.
+  int status = CSE_OK, err = CSE_OK;
   for (auto& s : m->shards) {
-    MD_HIP(hipSetDevice(s.device));
+    if (hipSetDevice(s.device) != hipSuccess) {
+      if (!err) err = CseFail(CSE_ERR_HIP, "hipSetDevice failed");
+      continue;
+    }
     const int rc = cse_wait(s.ev);
-    if (rc < 0) return rc;
+    if (rc < 0) {
+      if (!err) err = rc;
+      (void)hipStreamSynchronize(s.stream);
+      continue;
+    }
     if (rc == CSE_EVALUATION_FAILED) status = rc;
-    // Unregistered caller buffers: synchronous copies now.
+    if (err) continue;
+    // Caller buffers that are not page-locked: synchronous copies now.
     if (residuals && !async_res)
       for (const auto& iv : s.res_iv)
-        MD_HIP(hipMemcpy(residuals + iv.begin, s.d_res + iv.local, (iv.end - iv.begin) * sizeof(double),
-                         hipMemcpyDeviceToHost));
+        if (hipMemcpy(residuals + iv.begin, s.d_res + iv.local, (iv.end - iv.begin) * sizeof(double),
+                      hipMemcpyDeviceToHost) != hipSuccess && !err)
+          err = CseFail(CSE_ERR_HIP, "hipMemcpy (residual strip) failed");
     if (jac && !async_jac)
       for (const auto& iv : s.jac_iv)
-        MD_HIP(hipMemcpy(jac + iv.begin, s.d_jac + iv.local, (iv.end - iv.begin) * sizeof(double),
-                         hipMemcpyDeviceToHost));
+        if (hipMemcpy(jac + iv.begin, s.d_jac + iv.local, (iv.end - iv.begin) * sizeof(double),
+                      hipMemcpyDeviceToHost) != hipSuccess && !err)
+          err = CseFail(CSE_ERR_HIP, "hipMemcpy (Jacobian strip) failed");
+  }
+#undef MD_Q
+  if (err) {
+    m->state_current = false;
+    return err;
   }
   if (status != CSE_OK) return status;
   // Cost and gradient: sums over the shards in shard order.
@@ -541,7 +645,66 @@ int MultiSetPlusJacobians(CseMulti* m, const double* pj) {
 }
 
 int MultiPlus(CseMulti* m, const double* state, const double* delta, double* out) {
-  return cse_plus(m->shards[0].ev, state, delta, out);
+  // Each shard applies Plus to the parameter blocks it holds (a camera seen
+  // by several shards gets the same result from each); every active block
+  // belongs to some shard (MultiCreate).  Local slices through pinned
+  // staging, the shard's own cse_plus in between.
+  for (auto& s : m->shards) {
+    if (s.nstate == 0) continue;
+    MD_HIP(hipSetDevice(s.device));
+    if (!s.h_x) MD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_x), s.nstate * sizeof(double)));
+    if (!s.h_d)
+      MD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_d), std::max<int64_t>(s.ngrad, 1) * sizeof(double)));
+    if (!s.h_o) MD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_o), s.nstate * sizeof(double)));
+    for (const auto& iv : s.state_iv)
+      std::memcpy(s.h_x + iv.local, state + iv.begin, (iv.end - iv.begin) * sizeof(double));
+    for (const auto& iv : s.grad_iv)
+      std::memcpy(s.h_d + iv.local, delta + iv.begin, (iv.end - iv.begin) * sizeof(double));
+    const int rc = cse_plus(s.ev, s.h_x, s.h_d, s.h_o);
+    if (rc) return rc;
+    for (const auto& iv : s.state_iv)
+      std::memcpy(out + iv.begin, s.h_o + iv.local, (iv.end - iv.begin) * sizeof(double));
+  }
+  return CSE_OK;
+}
+
+int MultiTransferBytes(CseMulti* m, int64_t* state_h2d, int64_t* strips_d2h) {
+  for (size_t k = 0; k < m->shards.size(); ++k) {
+    const auto& s = m->shards[k];
+    if (state_h2d) state_h2d[k] = s.nstate * (int64_t)sizeof(double);
+    if (strips_d2h) strips_d2h[k] = (s.nres + s.njac) * (int64_t)sizeof(double);
+  }
+  return CSE_OK;
+}
+
+int CseHostRegister(void* p, size_t bytes) {
+  if (!p || bytes == 0) return CseFail(CSE_ERR_INVALID, "cse_host_register: empty range");
+  const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return CseFail(CSE_ERR_HIP, std::string("hipHostRegister: ") + hipGetErrorString(e));
+  }
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+  g_reg.push_back({b, b + bytes});
+  return CSE_OK;
+}
+
+int CseHostUnregister(void* p) {
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    const uintptr_t b = reinterpret_cast<uintptr_t>(p);
+    auto it = std::find_if(g_reg.begin(), g_reg.end(), [&](const auto& r) { return r.first == b; });
+    if (it == g_reg.end())
+      return CseFail(CSE_ERR_INVALID, "cse_host_unregister: not registered with cse_host_register");
+    g_reg.erase(it);
+  }
+  const hipError_t e = hipHostUnregister(p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return CseFail(CSE_ERR_HIP, std::string("hipHostUnregister: ") + hipGetErrorString(e));
+  }
+  return CSE_OK;
 }
 
 int MultiKernelStats(CseMulti* m, double* last_ms, double* total_ms, int64_t* launches) {

@@ -532,14 +532,24 @@ __global__ __launch_bounds__(kBlockThreads) void QuaternionPlusKernel(const doub
   const double* q = x + B.state_offset;
   const double* d = delta + B.delta_offset;
   double* o = out + B.state_offset;
-  const double n2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
-  if (n2 == 0.0) {
+  // |delta| as std::hypot(d0, d1, d2) (manifold.cc:33), in libstdc++'s
+  // scaled form: no underflow for tiny steps (|d| < 1e-154 would square to
+  // zero and be skipped), no overflow for huge ones; zero exactly when the
+  // three components are (the FP_ZERO test, :35).
+  const double a0 = fabs(d[0]), a1 = fabs(d[1]), a2 = fabs(d[2]);
+  const double m = fmax(a0, fmax(a1, a2));
+  if (m == 0.0) {
     o[0] = q[0];
     o[1] = q[1];
     o[2] = q[2];
     o[3] = q[3];
   } else {
-    const double nd = sqrt(n2);
+    double nd;
+    {
+#pragma clang fp contract(off)
+      const double r0 = a0 / m, r1 = a1 / m, r2 = a2 / m;
+      nd = m * sqrt(r0 * r0 + r1 * r1 + r2 * r2);
+    }
     double sn, cs;
     sincos(nd, &sn, &cs);
     const double sbd = sn / nd;

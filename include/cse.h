@@ -26,7 +26,10 @@
 extern "C" {
 #endif
 
-#define CSE_ABI_VERSION 1
+/* 2: cse_parameter_block.manifold (was `reserved`, which had to be 0),
+ *    cse_host_register / cse_host_unregister, cse_shard_transfer_bytes,
+ *    shard-local state in cse_create_multi. */
+#define CSE_ABI_VERSION 2
 
 /* Return codes. */
 #define CSE_OK 0
@@ -99,7 +102,7 @@ typedef struct cse_parameter_block {
   int32_t size;                 /* ambient size */
   int32_t tangent_size;         /* == size without a manifold */
   int32_t is_constant;          /* held constant: no Jacobian, no gradient */
-  int32_t manifold;             /* cse_manifold_kind */
+  int32_t manifold;             /* cse_manifold_kind (ABI 1: `reserved`, 0) */
   int64_t state_offset;         /* into state (active) / constant_state (constant) */
   int64_t delta_offset;         /* into the gradient (active only) */
   int64_t plus_jacobian_offset; /* into plus_jacobians (size x tangent row-major), -1 = none */
@@ -359,21 +362,26 @@ int cse_schur_back_substitute(cse_evaluator* ev, const double* d_x, double* d_y)
  * contiguous shards at point-bucket boundaries (a block whose last parameter
  * block differs from the previous block's; multiples of 4 blocks where
  * possible), each shard is evaluated on devices[k] (repeats allowed: several
- * shards on one device), and cse_evaluate on the returned handle
+ * shards on one device) holding only the parameter blocks its residual blocks
+ * use (a BAL shard: every camera it sees plus its own point slice), and
+ * cse_evaluate on the returned handle
+ *   - copies each shard's slices of the state to its device (only those
+ *     slices: cse_shard_transfer_bytes);
  *   - copies each shard's residual and Jacobian-value strips straight into
  *     disjoint regions of the caller's one residuals / jacobian_values
- *     buffers, concurrently per device (the buffers, and the state, are
- *     page-locked with hipHostRegister on first use and stay so until
- *     cse_destroy or until another buffer is passed in the same role);
+ *     buffers, concurrently per device when the buffers are page-locked
+ *     (cse_host_register, or the caller's own hipHostMalloc), synchronously
+ *     otherwise -- the library never pins a caller buffer by itself;
  *   - sums the cost and the gradient over the shards in shard order on the
  *     host (deterministic; a parameter block used by several shards, e.g. a
  *     camera, gets the sum of their rows).
+ * On an error every copy already queued is finished before the call returns.
  * options->use_stream and options->stream must be 0 (each device gets its
  * own stream).  On such a handle cse_evaluate, cse_wait (returns CSE_OK),
  * cse_plus, cse_set_plus_jacobians, cse_get_info (sizes of the whole
  * problem; bytes summed over the shards), cse_kernel_stats (the slowest
- * shard), cse_shard_info and cse_destroy work; the device-pointer entry
- * points return CSE_ERR_UNSUPPORTED. */
+ * shard), cse_shard_info, cse_shard_transfer_bytes and cse_destroy work; the
+ * device-pointer entry points return CSE_ERR_UNSUPPORTED. */
 int cse_create_multi(const cse_problem_desc* desc, const cse_options* options,
                      const int32_t* devices, int32_t num_devices, cse_evaluator** out);
 
@@ -382,6 +390,23 @@ int cse_create_multi(const cse_problem_desc* desc, const cse_options* options,
  * devices[num_shards] (may be NULL).  A cse_create evaluator has one shard. */
 int cse_shard_info(cse_evaluator* ev, int32_t* num_shards, int64_t* first_block,
                    int32_t* devices);
+
+/* Bytes one cse_evaluate moves per shard: state_h2d_bytes[num_shards] (the
+ * state slices the shard's device receives), strips_d2h_bytes[num_shards]
+ * (its residual and Jacobian-value strips); either may be NULL.  A cse_create
+ * evaluator has one shard (the whole state and outputs). */
+int cse_shard_transfer_bytes(cse_evaluator* ev, int64_t* state_h2d_bytes,
+                             int64_t* strips_d2h_bytes);
+
+/* Page-locks [p, p + bytes) of the caller's memory (hipHostRegister) for
+ * asynchronous copies until cse_host_unregister(p) with the same p; the
+ * multi-device evaluator then copies state slices and strips to and from
+ * buffers inside the range without staging.  The caller owns the range:
+ * unregister before freeing it.  (The reference pins inside its ContextImpl
+ * buffers, include/ceres/internal/cuda_buffer.h:98; here the caller's Ceres
+ * arrays are the transfer buffers.) */
+int cse_host_register(void* p, size_t bytes);
+int cse_host_unregister(void* p);
 
 void cse_destroy(cse_evaluator* ev);
 

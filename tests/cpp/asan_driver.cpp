@@ -249,6 +249,19 @@ static void RunFormat(const Bal& b, bool crs) {
     o.J.resize(sz.num_jacobian_values);
     for (int rep = 0; rep < 2; ++rep)
       EXPECT(cse_evaluate(ev, b.state.data(), &o.cost, o.r.data(), o.g.data(), o.J.data()) == CSE_OK);
+    if (multi) {
+      // The caller-pinned path (cse_host_register): asynchronous strips,
+      // the same values; per-shard transfer sizes.
+      EXPECT(cse_host_register(o.r.data(), o.r.size() * sizeof(double)) == CSE_OK);
+      EXPECT(cse_host_register(o.J.data(), o.J.size() * sizeof(double)) == CSE_OK);
+      EXPECT(cse_evaluate(ev, b.state.data(), &o.cost, o.r.data(), o.g.data(), o.J.data()) == CSE_OK);
+      EXPECT(cse_host_unregister(o.r.data()) == CSE_OK);
+      EXPECT(cse_host_unregister(o.J.data()) == CSE_OK);
+      EXPECT(cse_host_unregister(o.J.data()) == CSE_ERR_INVALID);
+      int64_t h2d[3] = {0, 0, 0}, d2h[3] = {0, 0, 0};
+      EXPECT(cse_shard_transfer_bytes(ev, h2d, d2h) == CSE_OK);
+      EXPECT(h2d[0] > 0 && h2d[0] < sz.num_parameters * 8 && d2h[0] > 0);
+    }
     EXPECT(std::fabs(o.cost - o1.cost) <= 1e-12 * std::fabs(o1.cost));
     EXPECT(IsApprox(o.r, o1.r, 1e-13));
     EXPECT(IsApprox(o.g, o1.g, 1e-13));

@@ -118,6 +118,27 @@ def test_held_quaternion_camera_on_its_manifold(gpu):
     assert_parity(got, ref, "quaternion held")
 
 
+@pytest.mark.parametrize("const", [(0,), (0, 8), (5,)])
+def test_held_camera_without_manifold_among_manifold_cameras(gpu, const):
+    """A held camera declared without the manifold (its own manifold is
+    irrelevant: it has no columns) while the active ones are on it.  The
+    slot-0 kind must follow the active cameras' manifold, including when the
+    group's block 0 has the held camera."""
+    prog = held(const=const, loss=ca.Loss.huber(1.0), quaternion_manifold=True, seed=21,
+                compile=False)
+    P = int(np.sum(prog.pb_size == 3))
+    for c in const:
+        prog.pb_manifold[P + c] = ca._cse.MANIFOLD_MATRIX
+        prog.pb_tangent[P + c] = 10
+    prog.compile(ca.BLOCK_SPARSE, num_eliminate_blocks=P)
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog)
+    assert info.num_affine_groups == 1
+    assert_parity(got, ref, ("held camera without manifold", const))
+    tab, _ = gpu_eval(prog, force_general_layout=True)
+    assert_parity(tab, ref, ("held camera without manifold, table", const))
+
+
 def test_held_cameras_jacobian_products(gpu):
     torch = pytest.importorskip("torch")
     from test_spmv_gpu import dense_jacobian

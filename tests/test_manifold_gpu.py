@@ -142,7 +142,8 @@ def quaternion_plus_reference(x, delta):
     QuaternionPlusImpl (internal/ceres/manifold.cc:28-59) states it."""
     out = x.copy()
     d = delta[:3]
-    nd = np.sqrt((d * d).sum())
+    m = np.abs(d).max()  # std::hypot(d0, d1, d2), libstdc++'s scaled form
+    nd = m * np.sqrt(((np.abs(d) / m) ** 2).sum()) if m != 0.0 else 0.0
     if nd != 0.0:
         s = np.sin(nd) / nd
         w, a, b, c = np.cos(nd), s * d[0], s * d[1], s * d[2]
@@ -174,6 +175,29 @@ def test_plus_on_the_quaternion_manifold(gpu):
     assert np.array_equal(got[:3 * P], want[:3 * P])
     assert np.array_equal(got[3 * P:3 * P + 10], want[3 * P:3 * P + 10])  # zero step: exact
     assert np.allclose(got, want, rtol=1e-14, atol=1e-15)
+
+
+def test_quaternion_plus_tiny_and_huge_steps(gpu):
+    """|delta| by the scaled hypot of the reference (std::hypot, manifold.cc:
+    33-35): a rotation step of 1e-160 is not lost to underflow (it squares
+    to zero), and one of 1e200 does not overflow to inf."""
+    prog = quat_program(seed=3)
+    P, C = 700, 16
+    delta = np.zeros(prog.num_effective_parameters)
+    steps = [np.array([1e-160, 0.0, 0.0]), np.array([3e-170, -4e-170, 0.0]),
+             np.array([1e200, 0.0, 0.0]), np.array([0.0, 0.0, 0.0]),
+             np.array([1e-310, 1e-310, 1e-310])]
+    for c, st in enumerate(steps):
+        delta[3 * P + 9 * c: 3 * P + 9 * c + 3] = st
+    ev = ca.Evaluator(prog)
+    got = ev.plus(prog.state, delta)
+    ev.close()
+    for c in range(len(steps)):
+        so, do = 3 * P + 10 * c, 3 * P + 9 * c
+        want = quaternion_plus_reference(prog.state[so:so + 10], delta[do:do + 9])
+        g = got[so:so + 10]
+        assert np.all(np.isfinite(g)), c
+        assert np.allclose(g, want, rtol=1e-14, atol=1e-300), (c, g, want)
 
 
 def test_bundle_adjuster_with_quaternion_manifolds(gpu):

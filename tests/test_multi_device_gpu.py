@@ -76,6 +76,50 @@ def test_multi_device_small_bal(gpu, fmt, nshards):
     assert_parity(a, ref)
 
 
+def test_multi_device_shard_local_state_and_registered_buffers(gpu):
+    """Each shard holds every camera it sees plus only its own point slice
+    (SURVEY.md §8(e)): its device receives C*72 + P_shard*24 bytes of state
+    per evaluation, not the whole state.  Buffers the caller page-locked
+    (cse_host_register) take the asynchronous copies, others synchronous
+    ones: both give the same bits.  Plus covers every parameter block."""
+    C, P, O_ = 20, 3001, 21113
+    prog = bal.synthetic_program((C, P, O_), loss=ca.Loss.huber(1.0), seed=8)
+    ref = oracle_eval(prog, threads=8)
+    n = 4
+    ev = ca.Evaluator(prog, devices=[0] * n)
+    first, _ = ev.shard_info()
+    h2d, d2h = ev.transfer_bytes()
+    pt = prog.groups[0].ids[:, 1]
+    for k in range(n):
+        b0, b1 = first[k], first[k + 1]
+        npts = len(np.unique(pt[b0:b1]))
+        ncam = len(np.unique(prog.groups[0].ids[b0:b1, 0]))
+        assert h2d[k] == 8 * (3 * npts + 9 * ncam), k
+        assert d2h[k] == 8 * (2 + 24) * (b1 - b0), k
+    assert h2d.sum() < 8 * prog.num_parameters + n * 8 * 9 * C
+    plain = ev.evaluate()
+    state = np.array(prog.state)
+    bufs = (np.empty(prog.num_residuals), np.empty(prog.num_effective_parameters),
+            np.empty(prog.num_jacobian_values))
+    for a in (state, bufs[0], bufs[2]):
+        ca.host_register(a)
+    try:
+        pinned = ev.evaluate(state, out=bufs)
+        again = ev.evaluate(state, out=bufs, new_evaluation_point=False)
+    finally:
+        for a in (state, bufs[0], bufs[2]):
+            ca.host_unregister(a)
+    with pytest.raises(RuntimeError, match="not registered"):
+        ca.host_unregister(state)
+    assert plain[1] == pinned[1] == again[1]
+    assert all(np.array_equal(x, y) for x, y in zip(plain[2:], pinned[2:]))
+    assert_parity(plain, ref, "shard-local multi")
+    delta = np.random.default_rng(1).normal(size=prog.num_effective_parameters)
+    out = ev.plus(prog.state, delta)
+    ev.close()
+    assert np.array_equal(out, prog.state + delta)
+
+
 def test_multi_device_every_output_combination(gpu):
     prog = bal.synthetic_program((12, 900, 5003), loss=ca.Loss.cauchy(2.0), seed=4)
     ref = oracle_eval(prog, threads=8)
