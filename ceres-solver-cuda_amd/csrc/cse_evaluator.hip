@@ -26,7 +26,7 @@
 #include "multi_device.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
-#include "pipeline_launch.h"
+#include "../../tools/tuning/pipeline_launch.h"  // tuning build only
 #endif
 
 namespace {
@@ -219,6 +219,9 @@ struct Group {
   DevBuf<double> sdata;
   DevBuf<int32_t> sid1;
   bool sorted_ready = false;
+  // The slot-1 copy at a 32-byte stride the points kernel writes for
+  // CameraGradientKernel (GroupArgs::ppad; allocated on first use).
+  DevBuf<double> ppad;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -1092,7 +1095,8 @@ int CamGradSortedInputs(Group& G, hipStream_t s) {
 constexpr int kCamGradWavesPerWg = CSE_CAMGRAD_W1 ? 1 : cse::kWavesPerBlock;
 
 // CameraGradientKernel: the per-chunk slot-0 sums into P.chunk_partial.
-int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hipStream_t s) {
+int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hipStream_t s,
+                           bool use_ppad = true) {
   const Group::GradPlan& P = G.grad[0];
   cse::CamGradArgs cg{};
   cg.state = state;
@@ -1112,6 +1116,10 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
     cg.packed0 = G.packed0.p;
     cg.packed_lo = G.slot0_lo;
     cg.packed_stride = G.packed_stride;
+  }
+  if (G.ppad.p && use_ppad) {  // written by the points kernel, queued before
+    cg.ppad = G.ppad.p;
+    cg.ppad_lo = G.grad[1].lo;
   }
   constexpr int W = kCamGradWavesPerWg;
   const dim3 grid((unsigned)((P.nchunks + W - 1) / W));
@@ -1317,6 +1325,11 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       a.gfused = d_grad;
       a.gside = G.gside.p;
       a.gcontrib = G.gcontrib.p;
+      if (recompute && CSE_POINT_COPY != 0 && G.shape.s1 == 3) {
+        if ((rc = G.ppad.ensure((size_t)G.grad[1].count * 4))) return rc;
+        a.ppad = G.ppad.p;
+        a.ppad_lo = G.grad[1].lo;
+      }
       fn = PickFused(G.kind, G.loss.kind, G.policy, recompute, G.const0);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
@@ -1340,7 +1353,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
         CSE_HIP(hipEventRecord(ev->fork, ev->stream));
         CSE_HIP(hipStreamWaitEvent(ev->side, ev->fork, 0));
         if (CSE_GRAD_CONCURRENT == 1) {
-          if ((rc = LaunchCameraGradKernel(ev, G, d_state, ev->side))) return rc;
+          if ((rc = LaunchCameraGradKernel(ev, G, d_state, ev->side, false))) return rc;
           CSE_HIP(hipEventRecord(ev->join, ev->side));
         }
       }
@@ -1348,7 +1361,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
     if (side && CSE_GRAD_CONCURRENT == 2) {  // queued behind the points kernel, low priority
-      const int rc = LaunchCameraGradKernel(ev, G, d_state, ev->side);
+      const int rc = LaunchCameraGradKernel(ev, G, d_state, ev->side, false);
       if (rc) return rc;
       CSE_HIP(hipEventRecord(ev->join, ev->side));
     }

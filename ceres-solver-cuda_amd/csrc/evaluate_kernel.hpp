@@ -22,6 +22,8 @@
 #ifndef CSE_EVALUATE_KERNEL_HPP_
 #define CSE_EVALUATE_KERNEL_HPP_
 
+#include <type_traits>
+
 #include "kernel_common.hpp"
 
 namespace cse {
@@ -346,7 +348,7 @@ struct FusedGrad {
   static constexpr int S0p = (S0 + 1) & ~1;
   double g0[S0p];
   double g1[4];  // S1 == 3 sums, then the id (exact as a double)
-  bool interior = false, writer = false;
+  bool interior = false, writer = false, run_end = false;
   int64_t entry = 0;
   int key = 0;
 
@@ -374,7 +376,7 @@ struct FusedGrad {
     key = active ? id1 : 0x7fffffff;
     SegmentedScan<S1>(g1, key, lane);
     const int knext = __shfl_down(key, 1, kWave);
-    const bool run_end = lane == nw - 1 || (lane < nw - 1 && knext != key);
+    run_end = active && (lane == nw - 1 || (lane < nw - 1 && knext != key));
     const int k0 = __shfl(key, 0, kWave);
     const int kl = __shfl(key, nw - 1, kWave);
     const bool single = k0 == kl;
@@ -386,6 +388,15 @@ struct FusedGrad {
     g1[3] = (double)key;
   }
 };
+
+// The points-only fused kernel writes the slot-1 copy for
+// CameraGradientKernel (GroupArgs::ppad): each point once per wave, by the
+// last lane of its run, from the values the wave loaded anyway (A/B builds:
+// -DCSE_POINT_COPY=0 leaves it out and the camera kernel gathers from the
+// state).
+#ifndef CSE_POINT_COPY
+#define CSE_POINT_COPY 1
+#endif
 
 // Can the wave take the back-to-back store tail?  Full chunk, 16-byte
 // pieces that tile every segment exactly, 16-byte-aligned destinations.
@@ -555,6 +566,15 @@ using PointsOnlyTune = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, 
 using ShippedTuneC0 = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 0, 0, true>;
 using PointsOnlyTuneC0 = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true, 0, 0, 0, true>;
 
+// The settings the product (libcse.so) may instantiate; anything else exists
+// only in the tuning build (-DCSE_TUNING: tools/ A/B runs), where the
+// diagnostic kDiag settings deliberately write wrong values.
+template <class T>
+constexpr bool kProductTune = std::is_same<T, ShippedTune>::value ||
+                              std::is_same<T, PointsOnlyTune>::value ||
+                              std::is_same<T, ShippedTuneC0>::value ||
+                              std::is_same<T, PointsOnlyTuneC0>::value;
+
 // Does the shipped BSM Jacobian kernel of kind K stage in two rounds (and so
 // fit 4 workgroups per CU)?
 template <class K>
@@ -577,6 +597,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = S0 + S1;
   static_assert(!MayLeaveOutputs<K>::value, "affine kernels: functors that assign every output");
+#ifndef CSE_TUNING
+  static_assert(kProductTune<T>, "libcse.so instantiates the shipped settings only (tuning build: -DCSE_TUNING)");
+#endif
   constexpr bool kLdsE = T::kLdsE || kCrs || !kJac;
   constexpr bool kTwo = T::kTwoRound && kJac && !kCrs && kLdsE && S1 > 0;
   // CRS rows staged in two halves of the wave (lanes [0, 32), then [32, 64)).
@@ -622,14 +645,17 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     } else {
       id = LoadIds<K>(a, i);
     }
-    if constexpr (T::kDiag == 2 || T::kDiag == 3) {
+#ifdef CSE_TUNING
+    if constexpr (T::kDiag == 2 || T::kDiag == 3) {  // diagnostic: no camera gather
       GatherDataAndSlot1<K, true>(a, i, id, &in);
       const double* row = a.packed0;
 #pragma unroll
       for (int k = 0; k < Tr::X0; ++k) in.x0[k] = row[k];
       in.id0 = id.x;
       in.id1 = id.y;
-    } else if constexpr (T::kEarlyObs || T::kRegGather ||
+    } else
+#endif
+    if constexpr (T::kEarlyObs || T::kRegGather ||
                          (!kJac && Tr::D == 2 && Tr::NB == 2 && T::kCamStride == 0 && !T::kDmaOwn)) {
       // Residual-only and cost-only evaluations issue the observation load
       // with the ids load (1.5-2 % faster, profiles/round2/s4h; the
@@ -644,7 +670,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(0);
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok;
-  if constexpr (T::kDiag == 1 || T::kDiag == 3) {
+#ifdef CSE_TUNING
+  if constexpr (T::kDiag == 1 || T::kDiag == 3) {  // diagnostic: a few additions, no functor
     double t = in.x1[0] + in.x1[S1 > 1 ? 1 : 0];
 #pragma unroll
     for (int k = 0; k < S0; ++k) t += in.x0[k];
@@ -655,7 +682,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 #pragma unroll
     for (int k = 0; k < NR * S1p; ++k) J1[k] = t * (k + 2);
     ok = true;
-  } else {
+  } else
+#endif
+  {
     ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
   }
   if (ok && a.check_finite) {
@@ -718,6 +747,15 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         double* e = a.gside + 4 * (2 * c + 1);
         e[0] = e[1] = e[2] = 0.0;
         e[3] = fg.g1[3];
+      }
+      if constexpr (T::kNoContrib && CSE_POINT_COPY != 0) {
+        if (a.ppad && fg.run_end) {
+          double* pc = a.ppad + 4LL * (in.id1 - a.ppad_lo);
+          pc[0] = in.x1[0];
+          pc[1] = in.x1[1];
+          pc[2] = in.x1[2];
+          pc[3] = 0.0;
+        }
       }
     }
     if (lane == 0) {
@@ -830,6 +868,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
     sp = a.gside + 4 * fg.entry;
   }
+  constexpr bool kPointCopy = kGradF && T::kNoContrib && CSE_POINT_COPY != 0;
+  cse_v4i pq[2];
+  double* pc = nullptr;
+  bool pc_write = false;
+  if constexpr (kPointCopy) {
+    if constexpr (Tr::S1 == 3) {
+      pq[0] = AsV4i(in.x1[0], in.x1[1]);
+      pq[1] = AsV4i(in.x1[2], 0.0);
+    }
+    pc_write = a.ppad != nullptr && fg.run_end;
+    pc = a.ppad + 4LL * (in.id1 - a.ppad_lo);
+  }
   if constexpr (kContrib) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -880,14 +930,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 
   // ---- every store of the wave, back to back ----
   auto store_f = [&]() {
-    if constexpr (T::kDiag == 4) return;
+#ifdef CSE_TUNING
+    if constexpr (T::kDiag == 4) return;  // diagnostic: no Jacobian stores
+#endif
     if (jac) {
       SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0), T::kFPol>(f0, f1, q0);
       if constexpr (kQ0 > 0) StoreNt16<0, T::kFPol>(flast, q0[kQ0 - 1]);
     }
   };
   auto store_e = [&]() {
-    if constexpr (T::kDiag == 4 || T::kDiag == 5) return;
+#ifdef CSE_TUNING
+    if constexpr (T::kDiag == 4 || T::kDiag == 5) return;  // diagnostic: no E stores
+#endif
     if constexpr (kQ1 > 0) {
       if (!jac) return;
       if constexpr (kLdsE) {
@@ -935,6 +989,12 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       StoreNt16<0, 1>(sp, sq[0]);
       StoreNt16<16, 1>(sp, sq[1]);
     }
+    if constexpr (kPointCopy) {
+      if (pc_write) {
+        StoreNt16<0, 1>(pc, pq[0]);
+        StoreNt16<16, 1>(pc, pq[1]);
+      }
+    }
   }
   // The cost partial (one per wave, lane 0) and the failure flag, last.
   if (lane == 0) {
@@ -950,6 +1010,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kContrib) KeepAlive<kGQ>(gq);
     KeepAlive<2>(sq);
     asm volatile("" ::"v"(cb0), "v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
+    if constexpr (kPointCopy) {
+      KeepAlive<2>(pq);
+      asm volatile("" ::"v"(pc));
+    }
   }
 }
 
@@ -1067,6 +1131,10 @@ struct CamGradArgs {
   const double* packed0;
   int32_t packed_lo;
   int32_t packed_stride;
+  // The points kernel's 32-byte-stride copy of slot 1 (GroupArgs::ppad), or
+  // null: gather from the state.
+  const double* ppad;
+  int32_t ppad_lo;
 };
 
 // r and the slot-0 Jacobian (NR x S0, row-major) of one block, the slot-1
@@ -1131,6 +1199,16 @@ __global__ __launch_bounds__(kWPB * kWave) void CameraGradientKernel(const CamGr
     for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int k = 0; k < D; ++k) d[u][k] = __builtin_nontemporal_load(g.sdata + qb[u] * D + k);
+      if constexpr (S1 == 3) {
+        if (g.ppad) {  // the 32-byte-stride copy: one sector per point
+          const double* p1 = g.ppad + 4LL * (g.sid1[qb[u]] - g.ppad_lo);
+          const double2 xy = *reinterpret_cast<const double2*>(p1);
+          x1[u][0] = xy.x;
+          x1[u][1] = xy.y;
+          x1[u][2] = p1[2];
+          continue;
+        }
+      }
       const double* p1 = g.state + g.state_base1 + (int64_t)S1 * g.sid1[qb[u]];
 #pragma unroll
       for (int k = 0; k < S1; ++k) x1[u][k] = p1[k];

@@ -80,6 +80,12 @@ struct GroupArgs {
   double* gfused;
   double* gside;
   double* gcontrib;
+  // The fused gradient's points-only form also leaves a copy of the slot-1
+  // blocks at a 32-byte stride, (x, y, z, 0) at ppad + 4 * (id - ppad_lo),
+  // for CameraGradientKernel's gather (one 64-byte sector per point); null =
+  // none.
+  double* ppad;
+  int32_t ppad_lo;
   LossParams loss;
   int apply_loss;
   int check_finite;

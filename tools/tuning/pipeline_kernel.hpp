@@ -37,7 +37,7 @@
 #ifndef CSE_PIPELINE_KERNEL_HPP_
 #define CSE_PIPELINE_KERNEL_HPP_
 
-#include "evaluate_kernel.hpp"
+#include "../../ceres-solver-cuda_amd/csrc/evaluate_kernel.hpp"
 
 namespace cse {
 
