@@ -208,8 +208,13 @@ struct Group {
   // the offset of its first F cell.
   bool const0 = false;
   DevBuf<uint32_t> act0;
-  DevBuf<int64_t> src0, fbase, delta0;
-  std::vector<int64_t> h_fbase;
+  DevBuf<int64_t> src0, fbase, delta0, look;
+  std::vector<int64_t> h_fbase, h_look;
+  // Blocks per wave of the group's Jacobian kernels (cse::kChunkC0 for
+  // const0 groups, else cse::kWave) and of the chunk geometry that last
+  // wrote the group's cost partials (a switch between the two clears them).
+  int chunk = cse::kWave;
+  int partials_chunk = cse::kWave;
   // Fused gradient (cse::FusedGrad): eligible groups, and their slot-1
   // boundary entries and slot-0 contributions (allocated on first use).
   bool fuse_ok = false;
@@ -286,7 +291,8 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (CSE_TWOROUND_W1 != 0) {
-    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    constexpr int kChunk = T::kConst0 ? cse::kChunkC0 : cse::kWave;
+    const int64_t chunks = (a.n + kChunk - 1) / kChunk;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundW1<K, L, Co, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
   } else {
@@ -352,7 +358,8 @@ void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 template <class K, int L, bool Crs, class T = cse::PointsOnlyTune>
 void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (CSE_FUSEDPOINTS_W1 != 0) {
-    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+    constexpr int kChunk = T::kConst0 ? cse::kChunkC0 : cse::kWave;
+    const int64_t chunks = (a.n + kChunk - 1) / kChunk;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPointsW1<K, L, Crs, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
   } else {
@@ -920,11 +927,13 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
       return !d->parameter_blocks[g.parameter_block_ids[i * k.nb]].is_constant;
     };
     const int64_t e0 = O[L[gidx(0)] + (act(0) ? NR : 0)];
-    std::vector<int64_t> fb;
-    fb.reserve((size_t)((n + cse::kWave - 1) / cse::kWave));
+    // Per chunk of cse::kChunkC0 blocks: its first F cell, then the end of
+    // the F cells; and the first block with an active camera after it.
+    std::vector<int64_t> fb, lk;
+    fb.reserve((size_t)((n + cse::kChunkC0 - 1) / cse::kChunkC0 + 1));
     int64_t rank = 0;
     for (int64_t i = 0; i < n; ++i) {
-      if (i % cse::kWave == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
+      if (i % cse::kChunkC0 == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
       const int64_t base = L[gidx(i)];
       int a = 0;
       if (act(i)) {
@@ -942,7 +951,17 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
     }
     G->jac_stride[0] = (int64_t)NR * S0;
     G->jac_stride[1] = (int64_t)NR * S1;
+    fb.push_back(f0 + (int64_t)NR * S0 * rank);
+    lk.assign(fb.size() - 1, -1);
+    int64_t next_active = -1;
+    for (int64_t i = n - 1, c = (int64_t)lk.size() - 1; c >= 0; --c) {
+      const int64_t lo = c * cse::kChunkC0;
+      lk[c] = next_active;
+      for (; i >= lo; --i)
+        if (act(i)) next_active = i;
+    }
     G->h_fbase = std::move(fb);
+    G->h_look = std::move(lk);
     return kAffinePacked;
   }
   for (int j = 0; j < k.nb; ++j)
@@ -1004,6 +1023,7 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.packed0_stride = G.packed_stride;
   a.act0_bits = G.act0.p;
   a.fbase = G.fbase.p;
+  a.look = G.look.p;
   a.delta0 = G.delta0.p;
   a.gindex = G.gindex.p;
   a.first = G.first;
@@ -1042,7 +1062,7 @@ int FoldTiming(cse_evaluator* ev) {
 // add the slot-1 boundary entries and the slot-0 contributions, per
 // parameter block in a fixed order, into out (delta offsets).
 int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
-  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
+  const int64_t entries = 2 * ((G.n + G.chunk - 1) / G.chunk);
   hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
                      dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
@@ -1151,7 +1171,7 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
 // entries, then the slot-0 rows from the chunk sums, in a fixed order.
 int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s) {
   const Group::GradPlan& P = G.grad[0];
-  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
+  const int64_t entries = 2 * ((G.n + G.chunk - 1) / G.chunk);
   hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
                      dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
@@ -1318,7 +1338,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     const bool recompute = fused && mode != 3;  // slot 0 by CameraGradientKernel
     cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
     if (fused) {
-      const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
+      const int64_t chunks = (G.n + G.chunk - 1) / G.chunk;
       int rc;
       if ((rc = G.gside.ensure((size_t)(2 * chunks * 4)))) return rc;
       if (!recompute && (rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
@@ -1357,6 +1377,16 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
           CSE_HIP(hipEventRecord(ev->join, ev->side));
         }
       }
+    }
+    if (G.const0) {
+      // The held-camera Jacobian kernels write ceil(n / kChunkC0) partials, the
+      // residual-only ones ceil(n / 64): after a switch to the smaller count
+      // the slots beyond it would keep the other kernel's values.
+      const int geometry = jets ? cse::kChunkC0 : cse::kWave;
+      if (geometry == cse::kWave && G.partials_chunk != cse::kWave)
+        CSE_HIP(hipMemsetAsync(ev->partials.p + G.partial_offset, 0,
+                               G.num_wg * cse::kWavesPerBlock * sizeof(double), ev->stream));
+      G.partials_chunk = geometry;
     }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
@@ -1606,7 +1636,8 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     if (G.const0) ev->any_general = true;
     if (!G.affine) ev->any_general = true;
     if (G.affine) {
-      const int64_t chunks = (g.num_blocks + cse::kWave - 1) / cse::kWave;
+      G.chunk = G.const0 ? cse::kChunkC0 : cse::kWave;
+      const int64_t chunks = (g.num_blocks + G.chunk - 1) / G.chunk;
       G.num_wg = std::max<int64_t>(1, (chunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock);
     } else {
       G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
@@ -1650,6 +1681,8 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       if ((rc = G.src0.upload(src.data(), src.size(), s))) return bail(rc);
       if ((rc = G.delta0.upload(dlt.data(), dlt.size(), s))) return bail(rc);
       if (!G.h_fbase.empty() && (rc = G.fbase.upload(G.h_fbase.data(), G.h_fbase.size(), s)))
+        return bail(rc);
+      if (!G.h_look.empty() && (rc = G.look.upload(G.h_look.data(), G.h_look.size(), s)))
         return bail(rc);
       if (hipStreamSynchronize(s) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "upload failed"));
     }

@@ -41,11 +41,15 @@ namespace cse {
 //   kConst0 (BlockSparseMatrix): lanes with a constant slot-0 block (act0
 //       false) have no F cell; the others' cells are packed in lane order from
 //       fbase[c] (chunk c).
+//       head_skip: the full chunks before this one took the sector-aligned
+//       tail of the held-camera kernels, which wrote this chunk's F cells up
+//       to the first 64-byte boundary; those bytes are skipped.
 template <class K, bool kJac, bool kCrs, bool kHalves = false, bool kConst0 = false>
 __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
                                               int64_t i0, int nw, const double* r,
                                               const double* J0, const double* J1,
-                                              bool act0 = true, int64_t c = 0) {
+                                              bool act0 = true, int64_t c = 0,
+                                              bool head_skip = false) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   constexpr int N = S0 + S1;
@@ -97,7 +101,14 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
           for (int q = 0; q < NR * S0; ++q) st[rank * NR * S0 + q] = J0[q];
         }
         __builtin_amdgcn_wave_barrier();
-        WaveStore(st, a.jacobian + a.fbase[c], __popcll(m) * NR * S0, lane);
+        const int cnt = __popcll(m) * NR * S0;
+        int skip = 0;
+        if (head_skip && c > 0) {
+          const uintptr_t A = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
+          skip = (int)((((A + 63) & ~(uintptr_t)63) - A) >> 3);
+          skip = skip < cnt ? skip : cnt;
+        }
+        WaveStore(st + skip, a.jacobian + a.fbase[c] + skip, cnt - skip, lane);
       } else {
         if (active) {
 #pragma unroll
@@ -485,6 +496,29 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
   }
 }
 
+// Held-camera groups (Tune::kConst0): may full chunks take the sector-aligned
+// tail?  The residual, E-cell and F-cell bases 16-byte aligned (the chunk
+// segments then start on 64-byte sectors when the bases do).
+__device__ __forceinline__ bool C0Aligned(const GroupArgs& a) {
+  uintptr_t m = 0;
+  if (a.residuals) m |= reinterpret_cast<uintptr_t>(a.residuals + a.res_base);
+  if (a.jacobian)
+    m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[1][0]) |
+         reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[0]);
+  return (m & 15) == 0;
+}
+
+// Pieces kJ.. of a wave segment as SegmentStoresFrom, lane `lane` of
+// instruction j storing only when its piece j * 64 + lane is below P.
+template <int kJ, int kCount>
+__device__ __forceinline__ void SegmentStoresMasked(double* b0, double* b1, const cse_v4i* q, int lane,
+                                                    int P) {
+  if constexpr (kJ < kCount) {
+    if (kJ * kWave + lane < P) StoreNt16<(kJ % 8) * 1024 - 4096>(kJ < 8 ? b0 : b1, q[kJ]);
+    SegmentStoresMasked<kJ + 1, kCount>(b0, b1, q, lane, P);
+  }
+}
+
 // Compile-time knobs of the affine kernel.  The product instantiates only
 // ShippedTune; other settings exist in the tuning build (-DCSE_TUNING,
 // tools/), never in libcse.so.
@@ -618,9 +652,14 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
   __shared__ double stage[kWPB][kWave * kStageLane];
 
+  // Held-camera groups: kChunkC0 blocks a wave, lane kChunkC0 evaluating the
+  // first block with an active camera after the chunk (its F cell's head
+  // completes this wave's last 64-byte sector).
+  constexpr bool kC0J = T::kConst0 && kJac;
+  constexpr int kChunk = kC0J ? kChunkC0 : kWave;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
-  const int64_t num_chunks = (a.n + kWave - 1) / kWave;
+  const int64_t num_chunks = (a.n + kChunk - 1) / kChunk;
   const int64_t wg = T::kXcdMap ? XcdContiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t c = wg * kWPB + wave;
   double* partial_dst = a.partials + c;
@@ -629,11 +668,14 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     return;
   }
   double* st = stage[wave];
-  const int64_t i0 = c * kWave;
+  const int64_t i0 = c * kChunk;
   const int64_t rem = a.n - i0;
-  const int nw = rem < kWave ? (int)rem : kWave;
+  const int nw = rem < kChunk ? (int)rem : kChunk;
   const bool active = lane < nw;
-  const int64_t i = active ? i0 + lane : a.n - 1;
+  int64_t look_i = -1;
+  if constexpr (kC0J) look_i = nw == kChunk ? a.look[c] : -1;
+  const bool look = kC0J && lane == kChunk && look_i >= 0;
+  const int64_t i = active ? i0 + lane : (look ? look_i : a.n - 1);
 
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(2);
   AffineInputs<K> in;
@@ -721,10 +763,174 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   FusedGrad<K> fg;
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
+  if constexpr (kC0J) {
+    if (nw == kChunk && C0Aligned(a)) {
+      // ---- held-camera groups, full chunk: sector-aligned windows ----
+      // F: this wave writes [W0, W1): from its first F cell rounded up to a
+      // 64-byte sector (the previous wave wrote the head) to the next chunk's
+      // first F cell rounded up (its head comes from the lookahead lane), so
+      // every store covers whole sectors wherever held blocks shifted the
+      // packed cells; E (48 B) and residuals (16 B) of 60 blocks are whole
+      // sectors by themselves.
+      static_assert(!kCrs && NR == 2 && S1 > 0, "held-camera tail: two-slot BlockSparseMatrix kinds");
+      constexpr int kF = NR * S0;                     // doubles per F cell
+      constexpr int kQF = (kChunkC0 * kF / 2 + 3 + kWave - 1) / kWave;
+      constexpr int kPE = kChunkC0 * NR * S1 / 2;     // E pieces of a chunk
+      constexpr int kQE = (kPE + kWave - 1) / kWave;
+      constexpr int kLdsPieces = kWave * kStageLane / 2;
+      static_assert(kChunkC0 % 4 == 0 && kQF <= 9, "F window: one or two base registers");
+      const bool jacw = a.jacobian != nullptr;
+      cse_v4i qf[kQF], qe[kQE];
+      double* wf0 = nullptr;
+      double* wf1 = nullptr;
+      double* we0 = nullptr;
+      int P = 0;
+      if (jacw) {
+        const uint64_t m = __ballot((active || look) && act0);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if ((active || look) && act0) {
+#pragma unroll
+          for (int q = 0; q < kF; ++q) st[rank * kF + q] = J0[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uintptr_t A0 = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
+        const uintptr_t A1 = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c + 1]);
+        const uintptr_t AE = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[num_chunks]);
+        const uintptr_t W0 = c == 0 ? A0 : ((A0 + 63) & ~(uintptr_t)63);
+        const uintptr_t W1 = A1 == AE ? A1 : ((A1 + 63) & ~(uintptr_t)63);
+        P = W1 > W0 ? (int)((W1 - W0) >> 4) : 0;
+        const int off = W1 > W0 ? (int)((W0 - A0) >> 4) : 0;
+        const double2* st2 = reinterpret_cast<const double2*>(st);
+#pragma unroll
+        for (int j = 0; j < kQF; ++j) {
+          int p = off + j * kWave + lane;
+          p = p < kLdsPieces ? p : kLdsPieces - 1;
+          const double2 v = st2[p];
+          qf[j] = AsV4i(v.x, v.y);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (active) {
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < kQE; ++j) {
+          int p = j * kWave + lane;
+          p = p < kPE ? p : kPE - 1;
+          const double2 v = st2[p];
+          qe[j] = AsV4i(v.x, v.y);
+        }
+        double* fw = reinterpret_cast<double*>(W0);
+        wf0 = fw + 2 * lane + 512;
+        wf1 = fw + 2 * lane + 1536;
+        we0 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0 + 2 * lane + 512;
+      }
+      const cse_v4i qr = AsV4i(r[0], r[1]);
+      double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;
+      cse_v4i sq[2], pq[2];
+      double *gp = nullptr, *sp = nullptr, *pc = nullptr;
+      bool pc_write = false;
+      constexpr bool kPointCopy = kGradF && T::kNoContrib && CSE_POINT_COPY != 0;
+      // gradient_mode 3: the slot-0 contributions J0^T r of the chunk's own
+      // blocks (10 doubles each, block order), staged like the cells.
+      constexpr bool kContribC0 = kGradF && !T::kNoContrib;
+      constexpr int kGQ = kContribC0 ? FusedGrad<K>::S0p / 2 : 1;  // pieces per block
+      constexpr int kPC = kChunkC0 * kGQ;
+      constexpr int kQC = kContribC0 ? (kPC + kWave - 1) / kWave : 1;
+      cse_v4i qc[kQC];
+      double* cb0 = nullptr;
+      if constexpr (kContribC0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (active) {
+#pragma unroll
+          for (int j = 0; j < kGQ; ++j)
+            reinterpret_cast<double2*>(st)[lane * kGQ + j] = make_double2(fg.g0[2 * j], fg.g0[2 * j + 1]);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < kQC; ++j) {
+          int p = j * kWave + lane;
+          p = p < kPC ? p : kPC - 1;
+          const double2 v = reinterpret_cast<const double2*>(st)[p];
+          qc[j] = AsV4i(v.x, v.y);
+        }
+        cb0 = a.gcontrib + (int64_t)(2 * kGQ) * i0 + 2 * lane + 512;
+      }
+      if constexpr (kGradF) {
+        sq[0] = AsV4i(fg.g1[0], fg.g1[1]);
+        sq[1] = AsV4i(fg.g1[2], fg.g1[3]);
+        gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
+        sp = a.gside + 4 * fg.entry;
+        if constexpr (kPointCopy) {
+          pq[0] = AsV4i(in.x1[0], in.x1[1]);
+          pq[1] = AsV4i(in.x1[2], 0.0);
+          pc_write = a.ppad != nullptr && fg.run_end;
+          pc = a.ppad + 4LL * (in.id1 - a.ppad_lo);
+        }
+      }
+      double* v_partial = partial_dst;
+      double v_wsum = wsum;
+      asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
+      asm volatile("" ::"v"(wf0), "v"(wf1), "v"(we0), "v"(rdst));
+      // ---- every store of the wave ----
+      if (jacw) {
+        SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
+        SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
+      }
+      if (a.residuals && active) StoreNt16<0>(rdst, qr);
+      if constexpr (kGradF) {
+        if constexpr (kContribC0) SegmentStoresMasked<0, kQC>(cb0, cb0, qc, lane, kPC);
+        if (fg.interior) {
+          StoreB64At<0>(gp, fg.g1[0]);
+          StoreB64At<8>(gp, fg.g1[1]);
+          StoreB64At<16>(gp, fg.g1[2]);
+        }
+        if (fg.writer) {
+          StoreNt16<0, 1>(sp, sq[0]);
+          StoreNt16<16, 1>(sp, sq[1]);
+        }
+        if constexpr (kPointCopy) {
+          if (pc_write) {
+            StoreNt16<0, 1>(pc, pq[0]);
+            StoreNt16<16, 1>(pc, pq[1]);
+          }
+        }
+      }
+      if (lane == 0) {
+        StoreB64(v_partial, v_wsum);
+        if (failed) StoreB32(status_dst, 1);
+      }
+      if constexpr (kContribC0) {
+        KeepAlive<kQC>(qc);
+        asm volatile("" ::"v"(cb0));
+      }
+      KeepAlive<kQF>(qf);
+      KeepAlive<kQE>(qe);
+      asm volatile("" ::"v"(qr), "v"(wf0), "v"(wf1), "v"(we0), "v"(rdst), "v"(v_partial), "v"(v_wsum));
+      if constexpr (kGradF) {
+        KeepAlive<2>(sq);
+        asm volatile("" ::"v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
+        if constexpr (kPointCopy) {
+          KeepAlive<2>(pq);
+          asm volatile("" ::"v"(pc));
+        }
+      }
+      return;
+    }
+  }
   bool fast = FastTail<K, kJac, kCrs, T::kConst0>(a, i0, nw, c);
-  if constexpr (T::kConst0) fast = fast && __ballot(!act0) == 0;
+  if constexpr (kC0J) fast = false;  // full aligned chunks returned above
   if (!fast) {
-    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
+    bool head_skip = false;
+    if constexpr (kC0J) head_skip = C0Aligned(a);
+    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c,
+                                                       head_skip);
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;

@@ -90,6 +90,45 @@ def test_held_cameras_ragged(gpu, n_obs):
     assert_parity(got, ref, n_obs)
 
 
+@pytest.mark.parametrize("n_obs", [600, 601, 658, 1200])
+@pytest.mark.parametrize("mode", [0, 3])
+def test_held_blocks_at_chunk_boundaries(gpu, n_obs, mode):
+    """The held-camera kernels cut the blocks into waves of 60 (cse::kChunkC0)
+    and each wave writes its F cells up to the next 64-byte sector, taking the
+    head of the next wave's first F cell from a lookahead lane.  Held blocks
+    right at and around the cuts (the lookahead then skips them), four in a
+    row, a wave whose cells start mid-sector, ragged ends: against the oracle
+    and bit-identical to the table path (residuals, Jacobian)."""
+    rng = np.random.default_rng(n_obs + mode)
+    C, P = 8, n_obs // 3
+    held_blocks = {0, 59, 60, 61, 119, 120, 179, 180, 181, 182, 183, 239, 299, 300, 301, 302,
+                   359, 420, 540, 541, 599, 600, 601, 659, 660, 1139, 1140, 1199}
+    ci = rng.integers(1, C, n_obs)
+    for b in held_blocks:
+        if b < n_obs:
+            ci[b] = 0
+    pi = np.arange(n_obs) * P // n_obs
+    cams, pts, _, _, _ = bal.synthetic(C, P, n_obs, seed=n_obs)
+    obs = bal.project(cams, pts, ci, pi) + rng.normal(0.0, 1.0, (n_obs, 2))
+    prog = bal.program(cams, pts, ci, pi, obs, loss=ca.Loss.huber(1.0), constant_cameras=(0,))
+    ref = oracle_eval(prog)
+    got, info = gpu_eval(prog, gradient_mode=mode)
+    assert info.num_affine_groups == 1
+    assert_parity(got, ref, ("chunk boundaries", n_obs, mode))
+    tab, _ = gpu_eval(prog, force_general_layout=True)
+    assert np.array_equal(got[2], tab[2]) and np.array_equal(got[4], tab[4])
+    # residual-only after the Jacobian evaluation on the same evaluator (the
+    # two kernels write different numbers of cost partials)
+    ev = ca.Evaluator(prog, gradient_mode=mode)
+    full = ev.evaluate()
+    res = ev.evaluate(residuals=True, gradient=False, jacobian=False)
+    cost = ev.evaluate(residuals=False, gradient=False, jacobian=False)
+    again = ev.evaluate()
+    ev.close()
+    assert abs(res[1] - full[1]) <= 1e-12 * abs(full[1]) and cost[1] == res[1]
+    assert again[1] == full[1] and np.array_equal(again[4], full[4])
+
+
 def test_chunks_whose_cameras_are_all_held(gpu):
     # Most cameras held: whole 64-block chunks without an F cell.
     prog = held(counts=(10, 2000, 9000), const=tuple(range(1, 10)), loss=ca.Loss.huber(1.0))
