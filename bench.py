@@ -480,6 +480,27 @@ def main():
                     "headline value)"}
         del hres, hjac
 
+        if world == 1 and args.config == "problem-13682-4456117" and not variant:
+            # BASELINE.json configs[2] (problem-1778, HuberLoss,
+            # CompressedRowSparseMatrix) in the same driver-timed run: its own
+            # evaluator, the same timed-loop rules as the headline.
+            c2 = bal.synthetic(*bal.CONFIGS["problem-1778-993923"], seed=args.seed)
+            se2 = distributed.ShardedEvaluator(*c2, 0, 1, device=dev_index, loss=ca.Loss.huber(1.0),
+                                               format=ca.COMPRESSED_ROW, gradient=False,
+                                               stream=stream)
+            del c2
+            info2 = se2.evaluator.info()
+            saved = se, ev
+            se, ev = se2, se2.evaluator  # run_leg times the evaluator held in `se`, `ev`
+            try:
+                leg("configs2", lambda: se2.evaluate(residuals=True, jacobian=True, gradient=False),
+                    info2.bytes_jacobian_eval, max(ks, 50),
+                    "BASELINE configs[2]: problem-1778-993923 (1,778 cameras, 993,923 points, "
+                    "5,001,946 blocks), SnavelyReprojectionError<2,9,3>, HuberLoss(1.0), "
+                    "CompressedRowSparseMatrix, residuals + Jacobian + cost, device-resident")
+            finally:
+                se, ev = saved
+                se2.close()
         if world == 1 and args.scaling == "strong":
             # The reference's seam served by one process over every visible
             # device (cse_create_multi): point-bucket shards, each device's

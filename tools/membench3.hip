@@ -132,7 +132,10 @@ __device__ __forceinline__ void Addr(Set* s, double* res, double* E, double* F, 
 }
 
 // ---- one chunk per wave (the shipped structure) ----------------------------
-template <int kFma>
+// kLoads: 2 the evaluator's loads (ids, then the camera DMA, observations
+// and point); 1 the ids only (the rest derived from them); 0 none (inputs
+// derived from the block index): what the load phase costs.
+template <int kFma, int kLoads = 2>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void onechunk(
     const int2* ids, const double2* obs, const double* pts, const double* cam, double* res, double* E,
     double* F, double* part, long n) {
@@ -141,26 +144,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void on
   const long c = blockIdx.x;
   long i = c * 64 + lane;
   if (i >= n) i = n - 1;
-  const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(ids) + i);
-  const int2 id = make_int2((int)b, (int)(b >> 32));
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int p = k * 64 + lane;
-    const int t = p / 5, q = p - t * 5;
-    const int cid = __shfl(id.x, t, 64);
-    __builtin_amdgcn_global_load_lds(cam + (long)kRow * cid + 2 * q, st + 128 * k, 16, 0, 0);
-  }
   double x[14];
-  x[12] = __builtin_nontemporal_load(reinterpret_cast<const double*>(obs) + 2 * i);
-  x[13] = __builtin_nontemporal_load(reinterpret_cast<const double*>(obs) + 2 * i + 1);
-  const double* pt = pts + 3L * id.y;
+  if constexpr (kLoads == 0) {
 #pragma unroll
-  for (int k = 0; k < 3; ++k) x[9 + k] = __builtin_nontemporal_load(pt + k);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
+    for (int k = 0; k < 14; ++k) x[k] = 1.0 + 1e-3 * (double)((i + k) & 1023);
+  } else {
+    const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(ids) + i);
+    const int2 id = make_int2((int)b, (int)(b >> 32));
+    if constexpr (kLoads == 1) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) x[k] = st[lane * 10 + k];
-  __builtin_amdgcn_wave_barrier();
+      for (int k = 0; k < 14; ++k) x[k] = 1.0 + 1e-3 * (double)((id.x + id.y + k) & 1023);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int p = k * 64 + lane;
+        const int t = p / 5, q = p - t * 5;
+        const int cid = __shfl(id.x, t, 64);
+        __builtin_amdgcn_global_load_lds(cam + (long)kRow * cid + 2 * q, st + 128 * k, 16, 0, 0);
+      }
+      x[12] = __builtin_nontemporal_load(reinterpret_cast<const double*>(obs) + 2 * i);
+      x[13] = __builtin_nontemporal_load(reinterpret_cast<const double*>(obs) + 2 * i + 1);
+      const double* pt = pts + 3L * id.y;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) x[9 + k] = __builtin_nontemporal_load(pt + k);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < 9; ++k) x[k] = st[lane * 10 + k];
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
   double J[26];
   Fake<kFma>(x, J);
   double w = J[0];
@@ -371,6 +384,9 @@ int main(int argc, char** argv) {
     run("persist fma702 8/CU", [&] { hipLaunchKernelGGL(persist<702>, dim3(pgrid(8)), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
     run("persist fma702 6/CU", [&] { hipLaunchKernelGGL(persist<702>, dim3(pgrid(6)), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
     run("persist fma702 4/CU", [&] { hipLaunchKernelGGL(persist<702>, dim3(pgrid(4)), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
+    run("onechunk fma702 ids-only", [&] { hipLaunchKernelGGL((onechunk<702, 1>), dim3(g1), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
+    run("onechunk fma702 no-loads", [&] { hipLaunchKernelGGL((onechunk<702, 0>), dim3(g1), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
+    run("onechunk fma0 no-loads", [&] { hipLaunchKernelGGL((onechunk<0, 0>), dim3(g1), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
     run("onechunk fma1404", [&] { hipLaunchKernelGGL(onechunk<1404>, dim3(g1), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
     run("persist fma1404 8/CU", [&] { hipLaunchKernelGGL(persist<1404>, dim3(pgrid(8)), dim3(64), 0, 0, ids, obs, pts, cam, res, E, F, part, (long)kO); });
   }
