@@ -332,11 +332,12 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
 #ifndef CSE_TWOROUNDCRS_W1
 #define CSE_TWOROUNDCRS_W1 1
 #endif
-template <class K, int L, int Co>
+template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  if constexpr (CSE_TWOROUNDCRS_W1 != 0) {
-    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-    hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrsW1<K, L, Co>), dim3((unsigned)chunks),
+  if constexpr (CSE_TWOROUNDCRS_W1 != 0 || T::kConst0) {
+    constexpr int kChunk = T::kConst0 ? cse::kChunkC0 : cse::kWave;
+    const int64_t chunks = (a.n + kChunk - 1) / kChunk;
+    hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrsW1<K, L, Co, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
   } else {
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrs<K, L, Co>), dim3((unsigned)num_wg),
@@ -389,17 +390,17 @@ LaunchFn PickFusedK(int loss, bool crs, bool points) {
   }
 }
 
-template <class K>
+template <class K, bool Crs>
 LaunchFn PickFusedC0(int loss, bool points) {
   using TP = cse::PointsOnlyTuneC0;
   using TF = cse::ShippedTuneC0;
   switch (loss) {
     case CSE_LOSS_HUBER:
-      return points ? &LaunchFusedPoints<K, cse::kLossHuber, false, TP> : &LaunchFused<K, cse::kLossHuber, false, TF>;
+      return points ? &LaunchFusedPoints<K, cse::kLossHuber, Crs, TP> : &LaunchFused<K, cse::kLossHuber, Crs, TF>;
     case CSE_LOSS_CAUCHY:
-      return points ? &LaunchFusedPoints<K, cse::kLossCauchy, false, TP> : &LaunchFused<K, cse::kLossCauchy, false, TF>;
+      return points ? &LaunchFusedPoints<K, cse::kLossCauchy, Crs, TP> : &LaunchFused<K, cse::kLossCauchy, Crs, TF>;
     default:
-      return points ? &LaunchFusedPoints<K, cse::kLossTrivial, false, TP> : &LaunchFused<K, cse::kLossTrivial, false, TF>;
+      return points ? &LaunchFusedPoints<K, cse::kLossTrivial, Crs, TP> : &LaunchFused<K, cse::kLossTrivial, Crs, TF>;
   }
 }
 
@@ -409,9 +410,11 @@ LaunchFn PickFusedC0(int loss, bool points) {
 LaunchFn PickFused(int kind, int loss, int policy, bool points, bool const0 = false) {
   const bool crs = policy == kAffineCrs;
   if (const0) {
-    if (crs) return nullptr;
-    if (kind == kKindQuaternionTangent) return PickFusedC0<cse::SnavelyQuaternionTangentKind>(loss, points);
-    return PickFusedC0<cse::SnavelyKind>(loss, points);
+    if (kind == kKindQuaternionTangent)
+      return crs ? PickFusedC0<cse::SnavelyQuaternionTangentKind, true>(loss, points)
+                 : PickFusedC0<cse::SnavelyQuaternionTangentKind, false>(loss, points);
+    return crs ? PickFusedC0<cse::SnavelyKind, true>(loss, points)
+               : PickFusedC0<cse::SnavelyKind, false>(loss, points);
   }
   if (kind == kKindQuaternionTangent)
     return PickFusedK<cse::SnavelyQuaternionTangentKind>(loss, crs, points);
@@ -544,16 +547,25 @@ LaunchFn TuningPick(int kind, int loss, bool jac, int policy, bool dma) {
 }
 #endif
 
-// const0: the group has constant slot-0 blocks (FusedKind kinds, BSM, the
-// repacked table; DetectAffine): the Jacobian kernel with the packed F cells.
-LaunchFn PickConst0(int kind, int loss, bool jac) {
+// const0: the group has constant slot-0 blocks (FusedKind kinds, the
+// repacked table; DetectAffine): the Jacobian kernel with the packed F cells
+// (BSM) or the packed row blocks of two widths (CRS).
+LaunchFn PickConst0(int kind, int loss, bool jac, bool crs) {
   auto pick = [&](auto kd) -> LaunchFn {
     using K = decltype(kd);
-    if (!jac) return nullptr;  // residual/cost kernels write no F cells: the usual ones
+    using T = cse::ShippedTuneC0;
+    if (!jac) return nullptr;  // residual/cost kernels write no Jacobian: the usual ones
+    if (crs) {
+      switch (loss) {
+        case CSE_LOSS_HUBER: return &LaunchTwoRoundCrs<K, cse::kLossHuber, 2, T>;
+        case CSE_LOSS_CAUCHY: return &LaunchTwoRoundCrs<K, cse::kLossCauchy, 2, T>;
+        default: return &LaunchTwoRoundCrs<K, cse::kLossTrivial, 2, T>;
+      }
+    }
     switch (loss) {
-      case CSE_LOSS_HUBER: return &LaunchTwoRound<K, cse::kLossHuber, 2, cse::ShippedTuneC0>;
-      case CSE_LOSS_CAUCHY: return &LaunchTwoRound<K, cse::kLossCauchy, 2, cse::ShippedTuneC0>;
-      default: return &LaunchTwoRound<K, cse::kLossTrivial, 2, cse::ShippedTuneC0>;
+      case CSE_LOSS_HUBER: return &LaunchTwoRound<K, cse::kLossHuber, 2, T>;
+      case CSE_LOSS_CAUCHY: return &LaunchTwoRound<K, cse::kLossCauchy, 2, T>;
+      default: return &LaunchTwoRound<K, cse::kLossTrivial, 2, T>;
     }
   };
   if (kind == kKindQuaternionTangent) return pick(cse::SnavelyQuaternionTangentKind{});
@@ -566,7 +578,10 @@ LaunchFn Pick(int kind, int loss, bool jac, int policy, bool dma, bool const0 = 
   if (!const0)
     if (LaunchFn f = TuningPick(kind, loss, jac, policy, dma)) return f;
 #endif
-  if (const0 && jac) return policy == kAffinePacked && dma ? PickConst0(kind, loss, jac) : nullptr;
+  if (const0 && jac)
+    return (policy == kAffinePacked || policy == kAffineCrs) && dma
+               ? PickConst0(kind, loss, jac, policy == kAffineCrs)
+               : nullptr;
   LaunchFn fn = nullptr;
   VisitKind(kind, [&](auto kd) {
     using K = decltype(kd);
@@ -917,52 +932,102 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
   const int64_t* L = d->jacobian_per_residual_layout;
   const int64_t* O = d->jacobian_per_residual_offsets;
   if (G->const0) {
-    // BlockSparseMatrix only: the E (slot 1) cells affine, kR x S1 packed at
-    // e0 + kR*S1*i; the F cells of the blocks with an active camera packed in
-    // block order from f0 (a constant camera has none; its block's first
-    // active entries are the E rows).
     const int NR = k.nr, S0 = sizes[0], S1 = sizes[1];
-    const int64_t f0 = O[L[gidx(first[0])]];
     auto act = [&](int64_t i) {
       return !d->parameter_blocks[g.parameter_block_ids[i * k.nb]].is_constant;
     };
-    const int64_t e0 = O[L[gidx(0)] + (act(0) ? NR : 0)];
-    // Per chunk of cse::kChunkC0 blocks: its first F cell, then the end of
-    // the F cells; and the first block with an active camera after it.
-    std::vector<int64_t> fb, lk;
-    fb.reserve((size_t)((n + cse::kChunkC0 - 1) / cse::kChunkC0 + 1));
-    int64_t rank = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      if (i % cse::kChunkC0 == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
-      const int64_t base = L[gidx(i)];
-      int a = 0;
-      if (act(i)) {
+    const int64_t nchunks = (n + cse::kChunkC0 - 1) / cse::kChunkC0;
+    // BlockSparseMatrix: the E (slot 1) cells affine, kR x S1 packed at
+    // e0 + kR*S1*i; the F cells of the blocks with an active camera packed in
+    // block order from f0 (a constant camera has none; its block's first
+    // active entries are the E rows).  Per chunk of cse::kChunkC0 blocks:
+    // its first F cell, then the end of the F cells; and the first block
+    // with an active camera after the chunk (the lookahead lane).
+    auto try_bsm = [&]() -> bool {
+      const int64_t f0 = O[L[gidx(first[0])]];
+      const int64_t e0 = O[L[gidx(0)] + (act(0) ? NR : 0)];
+      std::vector<int64_t> fb, lk;
+      fb.reserve((size_t)nchunks + 1);
+      int64_t rank = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        if (i % cse::kChunkC0 == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
+        const int64_t base = L[gidx(i)];
+        int a = 0;
+        if (act(i)) {
+          for (int r = 0; r < NR; ++r)
+            if (O[base + r] != f0 + (int64_t)NR * S0 * rank + (int64_t)r * S0) return false;
+          ++rank;
+          a = 1;
+        }
         for (int r = 0; r < NR; ++r)
-          if (O[base + r] != f0 + (int64_t)NR * S0 * rank + (int64_t)r * S0) return kTable;
-        ++rank;
-        a = 1;
+          if (O[base + a * NR + r] != e0 + (int64_t)NR * S1 * i + (int64_t)r * S1) return false;
       }
-      for (int r = 0; r < NR; ++r)
-        if (O[base + a * NR + r] != e0 + (int64_t)NR * S1 * i + (int64_t)r * S1) return kTable;
-    }
-    for (int r = 0; r < NR; ++r) {
-      G->jac_base[0][r] = f0 + (int64_t)r * S0;
-      G->jac_base[1][r] = e0 + (int64_t)r * S1;
-    }
-    G->jac_stride[0] = (int64_t)NR * S0;
-    G->jac_stride[1] = (int64_t)NR * S1;
-    fb.push_back(f0 + (int64_t)NR * S0 * rank);
-    lk.assign(fb.size() - 1, -1);
-    int64_t next_active = -1;
-    for (int64_t i = n - 1, c = (int64_t)lk.size() - 1; c >= 0; --c) {
-      const int64_t lo = c * cse::kChunkC0;
-      lk[c] = next_active;
-      for (; i >= lo; --i)
-        if (act(i)) next_active = i;
-    }
-    G->h_fbase = std::move(fb);
-    G->h_look = std::move(lk);
-    return kAffinePacked;
+      for (int r = 0; r < NR; ++r) {
+        G->jac_base[0][r] = f0 + (int64_t)r * S0;
+        G->jac_base[1][r] = e0 + (int64_t)r * S1;
+      }
+      G->jac_stride[0] = (int64_t)NR * S0;
+      G->jac_stride[1] = (int64_t)NR * S1;
+      fb.push_back(f0 + (int64_t)NR * S0 * rank);
+      lk.assign((size_t)nchunks, -1);
+      int64_t next_active = -1;
+      for (int64_t i = n - 1, c = nchunks - 1; c >= 0; --c) {
+        const int64_t lo = c * cse::kChunkC0;
+        lk[c] = next_active;
+        for (; i >= lo; --i)
+          if (act(i)) next_active = i;
+      }
+      G->h_fbase = std::move(fb);
+      G->h_look = std::move(lk);
+      return true;
+    };
+    // CompressedRowSparseMatrix (compressed_row_jacobian_writer.cc:145-185):
+    // every block's rows packed in block order, NR x (S0 + S1) with an active
+    // camera (camera and point at fixed columns of the row) and NR x S1 with
+    // a held one (the point alone).  Per chunk: the offset of its first row,
+    // then the end; the lookahead lane takes the next chunk's first block.
+    auto try_crs = [&]() -> bool {
+      const int N = S0 + S1;
+      const int64_t b0 = L[gidx(first[0])];
+      const int64_t cam0 = O[b0], pt0 = O[b0 + NR];
+      const int64_t rb0 = std::min(cam0, pt0);
+      const int camcol = (int)(cam0 - rb0), ptcol = (int)(pt0 - rb0);
+      if (!((camcol == 0 && ptcol == S0) || (ptcol == 0 && camcol == S1))) return false;
+      const int64_t r0 = rb0 - (int64_t)NR * S1 * first[0];
+      std::vector<int64_t> cb, lk;
+      cb.reserve((size_t)nchunks + 1);
+      int64_t pos = r0;
+      for (int64_t i = 0; i < n; ++i) {
+        if (i % cse::kChunkC0 == 0) cb.push_back(pos);
+        const int64_t base = L[gidx(i)];
+        if (act(i)) {
+          for (int r = 0; r < NR; ++r)
+            if (O[base + r] != pos + (int64_t)r * N + camcol ||
+                O[base + NR + r] != pos + (int64_t)r * N + ptcol)
+              return false;
+          pos += (int64_t)NR * N;
+        } else {
+          for (int r = 0; r < NR; ++r)
+            if (O[base + r] != pos + (int64_t)r * S1) return false;
+          pos += (int64_t)NR * S1;
+        }
+      }
+      cb.push_back(pos);
+      lk.assign((size_t)nchunks, -1);
+      for (int64_t c = 0; c < nchunks; ++c)
+        lk[c] = (c + 1) * cse::kChunkC0 < n ? (c + 1) * cse::kChunkC0 : -1;
+      for (int r = 0; r < NR; ++r) {
+        G->jac_base[0][r] = r0 + (int64_t)r * N + camcol;
+        G->jac_base[1][r] = r0 + (int64_t)r * N + ptcol;
+      }
+      G->jac_stride[0] = G->jac_stride[1] = (int64_t)NR * N;
+      G->h_fbase = std::move(cb);
+      G->h_look = std::move(lk);
+      return true;
+    };
+    if (try_bsm()) return kAffinePacked;
+    if (try_crs()) return kAffineCrs;
+    return kTable;
   }
   for (int j = 0; j < k.nb; ++j)
     for (int r = 0; r < k.nr; ++r) G->jac_base[j][r] = O[L[gidx(0)] + j * k.nr + r];

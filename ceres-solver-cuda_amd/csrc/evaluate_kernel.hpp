@@ -61,7 +61,52 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
   }
   if constexpr (kJac) {
     if (!a.jacobian) return;
-    if constexpr (kCrs) {
+    if constexpr (kCrs && kConst0) {
+      // Held cameras, CompressedRowSparseMatrix: the chunk's row blocks are
+      // packed from fbase[c] (NR x N with an active camera, NR x S1 with a
+      // held one); each lane writes its own (the slow tail: ragged or
+      // unaligned chunks), past the head a previous sector-aligned wave wrote.
+      static_assert(NB == 2, "two slots");
+      const uint64_t m_any = __ballot(active), m_act = __ballot(active && act0);
+      auto below = [&](uint64_t mm) {
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+      };
+      const int ob = NR * S1 * below(m_any) + NR * S0 * below(m_act);
+      int skip = 0;
+      if (head_skip && c > 0) {
+        const uintptr_t A = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
+        skip = (int)((((A + 63) & ~(uintptr_t)63) - A) >> 3);
+      }
+      if (active) {
+        double* seg = a.jacobian + a.fbase[c];
+        const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
+        const int camcol = (int)(a.jac_base[0][0] - row0), ptcol = (int)(a.jac_base[1][0] - row0);
+        if (act0) {
+#pragma unroll
+          for (int k = 0; k < NR; ++k) {
+#pragma unroll
+            for (int cc = 0; cc < S0; ++cc) {
+              const int o = ob + k * N + camcol + cc;
+              if (o >= skip) seg[o] = J0[k * S0 + cc];
+            }
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) {
+              const int o = ob + k * N + ptcol + cc;
+              if (o >= skip) seg[o] = J1[k * S1p + cc];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int cc = 0; cc < S1; ++cc) {
+              const int o = ob + k * S1 + cc;
+              if (o >= skip) seg[o] = J1[k * S1p + cc];
+            }
+        }
+      }
+    } else if constexpr (kCrs) {
       const int64_t row0 = a.jac_base[0][0] < a.jac_base[NB - 1][0] ? a.jac_base[0][0]
                                                                       : a.jac_base[NB - 1][0];
       constexpr int kParts = kHalves ? 2 : 1, kLanes = kWave / kParts;
@@ -738,7 +783,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
   bool act0 = true;  // slot-0 block active (T::kConst0: from its bit)
   if constexpr (T::kConst0) {
-    static_assert(!kCrs && kCoop == 2, "constant slot-0 blocks: BlockSparseMatrix, repacked table");
+    static_assert(kCoop == 2, "constant slot-0 blocks: the repacked table");
     if constexpr ((Tr::X0 & 1) != 0 && !T::kDmaOwn) {
       act0 = in.x0pad == 0.0;  // the flag came with the row (RepackSlot0Kernel)
     } else {
@@ -772,13 +817,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       // every store covers whole sectors wherever held blocks shifted the
       // packed cells; E (48 B) and residuals (16 B) of 60 blocks are whole
       // sectors by themselves.
-      static_assert(!kCrs && NR == 2 && S1 > 0, "held-camera tail: two-slot BlockSparseMatrix kinds");
-      constexpr int kF = NR * S0;                     // doubles per F cell
-      constexpr int kQF = (kChunkC0 * kF / 2 + 3 + kWave - 1) / kWave;
-      constexpr int kPE = kChunkC0 * NR * S1 / 2;     // E pieces of a chunk
-      constexpr int kQE = (kPE + kWave - 1) / kWave;
+      static_assert(NR == 2 && S1 > 0, "held-camera tail: two-slot kinds, two residuals");
+      constexpr int kF = NR * S0;  // doubles per F cell (BSM); a row block's camera part (CRS)
+      // BlockSparseMatrix: the F window (up to 60 cells and the head of the
+      // next), then the E cells.  CompressedRowSparseMatrix: one window over
+      // the chunk's row blocks (NR x (S1 + S0) with an active camera, NR x S1
+      // with a held one), staged in two halves of the wave.
+      constexpr int kSegPieces = kCrs ? kChunkC0 * NR * (S0 + S1) / 2 : kChunkC0 * kF / 2;
+      constexpr int kQF = (kSegPieces + 3 + kWave - 1) / kWave;
+      constexpr int kPE = kCrs ? 0 : kChunkC0 * NR * S1 / 2;  // E pieces of a chunk (BSM)
+      constexpr int kQE = kCrs ? 1 : (kPE + kWave - 1) / kWave;
       constexpr int kLdsPieces = kWave * kStageLane / 2;
-      static_assert(kChunkC0 % 4 == 0 && kQF <= 9, "F window: one or two base registers");
+      static_assert(kChunkC0 % 4 == 0 && kQF <= 16, "window: one or two base registers");
       const bool jacw = a.jacobian != nullptr;
       cse_v4i qf[kQF], qe[kQE];
       double* wf0 = nullptr;
@@ -786,14 +836,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       double* we0 = nullptr;
       int P = 0;
       if (jacw) {
-        const uint64_t m = __ballot((active || look) && act0);
-        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if ((active || look) && act0) {
-#pragma unroll
-          for (int q = 0; q < kF; ++q) st[rank * kF + q] = J0[q];
-        }
-        __builtin_amdgcn_wave_barrier();
         const uintptr_t A0 = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
         const uintptr_t A1 = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c + 1]);
         const uintptr_t AE = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[num_chunks]);
@@ -802,33 +844,92 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         P = W1 > W0 ? (int)((W1 - W0) >> 4) : 0;
         const int off = W1 > W0 ? (int)((W0 - A0) >> 4) : 0;
         const double2* st2 = reinterpret_cast<const double2*>(st);
+        if constexpr (kCrs) {
+          constexpr int N = S0 + S1;
+          const bool out = active || look;
+          const uint64_t m_any = __ballot(out), m_act = __ballot(out && act0);
+          auto below = [&](uint64_t mm) {
+            return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+          };
+          // this lane's row block inside the chunk's segment (doubles)
+          const int ob = NR * S1 * below(m_any) + NR * S0 * below(m_act);
+          const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
+          const int camcol = (int)(a.jac_base[0][0] - row0), ptcol = (int)(a.jac_base[1][0] - row0);
+          constexpr int kHalf = kChunkC0 / 2;
+          const int split = __builtin_amdgcn_readlane(ob, kHalf);  // where lane kHalf's block starts
+          const int total = __builtin_amdgcn_readlane(ob, kWave - 1);
 #pragma unroll
-        for (int j = 0; j < kQF; ++j) {
-          int p = off + j * kWave + lane;
-          p = p < kLdsPieces ? p : kLdsPieces - 1;
-          const double2 v = st2[p];
-          qf[j] = AsV4i(v.x, v.y);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (active) {
+          for (int h = 0; h < 2; ++h) {
+            const int lo = h == 0 ? 0 : split, hi = h == 0 ? split : total;
+            if (out && (h == 0 ? lane < kHalf : lane >= kHalf)) {
+              double* blk = st + (ob - lo);
+              if (act0) {
 #pragma unroll
-          for (int k = 0; k < NR; ++k)
+                for (int k = 0; k < NR; ++k) {
 #pragma unroll
-            for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
-        }
-        __builtin_amdgcn_wave_barrier();
+                  for (int cc = 0; cc < S0; ++cc) blk[k * N + camcol + cc] = J0[k * S0 + cc];
 #pragma unroll
-        for (int j = 0; j < kQE; ++j) {
-          int p = j * kWave + lane;
-          p = p < kPE ? p : kPE - 1;
-          const double2 v = st2[p];
-          qe[j] = AsV4i(v.x, v.y);
+                  for (int cc = 0; cc < S1; ++cc) blk[k * N + ptcol + cc] = J1[k * S1p + cc];
+                }
+              } else {
+#pragma unroll
+                for (int k = 0; k < NR; ++k)
+#pragma unroll
+                  for (int cc = 0; cc < S1; ++cc) blk[k * S1 + cc] = J1[k * S1p + cc];
+              }
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < kQF; ++j) {
+              const int o = 2 * (off + j * kWave + lane);  // segment offset, doubles (even)
+              if (o >= lo && o < hi) {
+                int p = (o - lo) >> 1;
+                p = p < kLdsPieces ? p : kLdsPieces - 1;
+                const double2 v = st2[p];
+                qf[j] = AsV4i(v.x, v.y);
+              }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+          }
+        } else {
+          const uint64_t m = __ballot((active || look) && act0);
+          const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if ((active || look) && act0) {
+#pragma unroll
+            for (int q = 0; q < kF; ++q) st[rank * kF + q] = J0[q];
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int j = 0; j < kQF; ++j) {
+            int p = off + j * kWave + lane;
+            p = p < kLdsPieces ? p : kLdsPieces - 1;
+            const double2 v = st2[p];
+            qf[j] = AsV4i(v.x, v.y);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          if (active) {
+#pragma unroll
+            for (int k = 0; k < NR; ++k)
+#pragma unroll
+              for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int j = 0; j < kQE; ++j) {
+            int p = j * kWave + lane;
+            p = p < kPE ? p : kPE - 1;
+            const double2 v = st2[p];
+            qe[j] = AsV4i(v.x, v.y);
+          }
+          we0 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0 + 2 * lane + 512;
         }
         double* fw = reinterpret_cast<double*>(W0);
         wf0 = fw + 2 * lane + 512;
         wf1 = fw + 2 * lane + 1536;
-        we0 = a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * i0 + 2 * lane + 512;
       }
       const cse_v4i qr = AsV4i(r[0], r[1]);
       double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;
@@ -881,7 +982,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       // ---- every store of the wave ----
       if (jacw) {
         SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
-        SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
+        if constexpr (!kCrs) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
       }
       if (a.residuals && active) StoreNt16<0>(rdst, qr);
       if constexpr (kGradF) {
@@ -1262,10 +1363,10 @@ __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound
   AffineChunkBody<K, kLoss, true, true, kCoop, false, ShippedTune>(a);
 }
 // The same with one wave per workgroup (6 KiB of LDS each).
-template <class K, int kLoss, int kCoop>
+template <class K, int kLoss, int kCoop, class T = ShippedTune>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 EvaluateAffineChunksTwoRoundCrsW1(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, true, true, kCoop, false, ShippedTune, 1>(a);
+  AffineChunkBody<K, kLoss, true, true, kCoop, false, T, 1>(a);
 }
 
 // The same held to at least kMinWaves waves per SIMD (a register bound:

@@ -5,11 +5,11 @@ bundle adjustment -- removes its columns: in the BlockSparseMatrix the blocks
 of that camera have no F cell, so every later block's F cell moves up by one
 cell (block_jacobian_writer.cc:75-149), and the camera's values come from the
 constant state (registered_cuda_evaluators.cc:237-248).  Groups whose slot-0
-blocks are partly constant stay on the affine kernels
-(cse::ShippedTuneC0: F cells packed in block order from a per-chunk base, waves
-with a held camera through the slow tail); CompressedRowSparseMatrix falls
-back to the table path.  Against the oracle (tests/parity_util.py
-tolerances): both layouts, losses, the four gradient modes, residual/cost-only,
+blocks are partly constant stay on the affine kernels (cse::ShippedTuneC0:
+F cells packed in block order from a per-chunk base, 60-block waves whose
+stores cover whole 64-byte sectors); the same for CompressedRowSparseMatrix,
+whose row blocks then have two widths.  Against the oracle
+(tests/parity_util.py tolerances): both layouts, losses, the four gradient modes, residual/cost-only,
 ragged sizes, whole chunks of held cameras, the quaternion manifold, the
 Jacobian products and the multi-device evaluator; the reference's own mix is
 the mini-BA of evaluator_cuda_test.cu.cc:232-459 (test_parity_gpu.py).
@@ -60,12 +60,21 @@ def test_held_cameras_bsm_affine(gpu, const, loss):
     assert np.array_equal(got[2], tab[2]) and np.array_equal(got[4], tab[4])
 
 
-def test_held_cameras_crs_takes_the_table_path(gpu):
-    prog = held(const=(2, 5), loss=ca.Loss.huber(1.0), fmt=ca.COMPRESSED_ROW)
+@pytest.mark.parametrize("const", [(2, 5), (0,), (15,), (0, 3, 9, 15)])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_held_cameras_crs_affine(gpu, const, mode):
+    """CompressedRowSparseMatrix with held cameras: row blocks of two widths
+    (NR x 12 with an active camera, NR x 3 with a held one) packed in block
+    order (compressed_row_jacobian_writer.cc:145-185), on the affine kernels."""
+    prog = held(const=const, loss=ca.Loss.huber(1.0), fmt=ca.COMPRESSED_ROW)
     ref = oracle_eval(prog)
-    got, info = gpu_eval(prog)
+    got, info = gpu_eval(prog, gradient_mode=mode)
+    assert info.num_affine_groups == 1
+    assert info.num_fused_gradient_groups == (0 if mode == 2 else 1)
+    assert_parity(got, ref, ("crs", const, mode))
+    tab, info = gpu_eval(prog, force_general_layout=True)
     assert info.num_affine_groups == 0
-    assert_parity(got, ref, "crs")
+    assert np.array_equal(got[2], tab[2]) and np.array_equal(got[4], tab[4])
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
@@ -90,9 +99,10 @@ def test_held_cameras_ragged(gpu, n_obs):
     assert_parity(got, ref, n_obs)
 
 
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
 @pytest.mark.parametrize("n_obs", [600, 601, 658, 1200])
 @pytest.mark.parametrize("mode", [0, 3])
-def test_held_blocks_at_chunk_boundaries(gpu, n_obs, mode):
+def test_held_blocks_at_chunk_boundaries(gpu, n_obs, mode, fmt):
     """The held-camera kernels cut the blocks into waves of 60 (cse::kChunkC0)
     and each wave writes its F cells up to the next 64-byte sector, taking the
     head of the next wave's first F cell from a lookahead lane.  Held blocks
@@ -110,11 +120,12 @@ def test_held_blocks_at_chunk_boundaries(gpu, n_obs, mode):
     pi = np.arange(n_obs) * P // n_obs
     cams, pts, _, _, _ = bal.synthetic(C, P, n_obs, seed=n_obs)
     obs = bal.project(cams, pts, ci, pi) + rng.normal(0.0, 1.0, (n_obs, 2))
-    prog = bal.program(cams, pts, ci, pi, obs, loss=ca.Loss.huber(1.0), constant_cameras=(0,))
+    prog = bal.program(cams, pts, ci, pi, obs, loss=ca.Loss.huber(1.0), constant_cameras=(0,),
+                       format=fmt)
     ref = oracle_eval(prog)
     got, info = gpu_eval(prog, gradient_mode=mode)
     assert info.num_affine_groups == 1
-    assert_parity(got, ref, ("chunk boundaries", n_obs, mode))
+    assert_parity(got, ref, ("chunk boundaries", n_obs, mode, fmt))
     tab, _ = gpu_eval(prog, force_general_layout=True)
     assert np.array_equal(got[2], tab[2]) and np.array_equal(got[4], tab[4])
     # residual-only after the Jacobian evaluation on the same evaluator (the
