@@ -24,6 +24,7 @@
 
 #include "../../include/cse.h"
 #include "multi_device.h"
+#include "persistent_launch.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
 #include "../../tools/tuning/pipeline_launch.h"  // tuning build only
@@ -208,13 +209,12 @@ struct Group {
   // the offset of its first F cell.
   bool const0 = false;
   DevBuf<uint32_t> act0;
-  DevBuf<int64_t> src0, fbase, delta0, look;
-  std::vector<int64_t> h_fbase, h_look;
-  // Blocks per wave of the group's Jacobian kernels (cse::kChunkC0 for
-  // const0 groups, else cse::kWave) and of the chunk geometry that last
-  // wrote the group's cost partials (a switch between the two clears them).
-  int chunk = cse::kWave;
-  int partials_chunk = cse::kWave;
+  DevBuf<int64_t> src0, fbase, delta0;
+  std::vector<int64_t> h_fbase;
+  // Held-camera sectors (HeldSectorFixupKernel): each chunk's two side
+  // slots and the previous chunk with F cells (BSM) or row blocks (CRS).
+  DevBuf<double> side;
+  DevBuf<int32_t> prev_seg;
   // Fused gradient (cse::FusedGrad): eligible groups, and their slot-1
   // boundary entries and slot-0 contributions (allocated on first use).
   bool fuse_ok = false;
@@ -291,8 +291,7 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (CSE_TWOROUND_W1 != 0) {
-    constexpr int kChunk = T::kConst0 ? cse::kChunkC0 : cse::kWave;
-    const int64_t chunks = (a.n + kChunk - 1) / kChunk;
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundW1<K, L, Co, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
   } else {
@@ -335,8 +334,7 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (CSE_TWOROUNDCRS_W1 != 0 || T::kConst0) {
-    constexpr int kChunk = T::kConst0 ? cse::kChunkC0 : cse::kWave;
-    const int64_t chunks = (a.n + kChunk - 1) / kChunk;
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrsW1<K, L, Co, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
   } else {
@@ -359,13 +357,34 @@ void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 template <class K, int L, bool Crs, class T = cse::PointsOnlyTune>
 void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (CSE_FUSEDPOINTS_W1 != 0) {
-    constexpr int kChunk = T::kConst0 ? cse::kChunkC0 : cse::kWave;
-    const int64_t chunks = (a.n + kChunk - 1) / kChunk;
+    const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPointsW1<K, L, Crs, T>), dim3((unsigned)chunks),
                        dim3(cse::kWave), 0, s, a);
   } else {
     hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs, T>), dim3((unsigned)num_wg),
                        dim3(cse::kBlockThreads), 0, s, a);
+  }
+}
+
+// The BlockSparseMatrix Jacobian evaluation of the Snavely camera
+// (residuals and Jacobian, no gradient, no held cameras) as persistent
+// software-pipelined waves (persistent_kernel.hpp, its own TU
+// persistent.hip): CSE_PERSISTENT 1; 0 keeps the one-chunk-per-wave kernel.
+#ifndef CSE_PERSISTENT
+#define CSE_PERSISTENT 0
+#endif
+template <int L>
+void LaunchPersistent(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  (void)num_wg;
+  cse::LaunchPersistentSnavely<L>(a, s);
+}
+
+LaunchFn PickPersistent(int kind, int loss) {
+  if (kind != CSE_FUNCTOR_SNAVELY_2_9_3) return nullptr;
+  switch (loss) {
+    case CSE_LOSS_HUBER: return &LaunchPersistent<cse::kLossHuber>;
+    case CSE_LOSS_CAUCHY: return &LaunchPersistent<cse::kLossCauchy>;
+    default: return &LaunchPersistent<cse::kLossTrivial>;
   }
 }
 
@@ -936,21 +955,20 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
     auto act = [&](int64_t i) {
       return !d->parameter_blocks[g.parameter_block_ids[i * k.nb]].is_constant;
     };
-    const int64_t nchunks = (n + cse::kChunkC0 - 1) / cse::kChunkC0;
+    const int64_t nchunks = (n + cse::kWave - 1) / cse::kWave;
     // BlockSparseMatrix: the E (slot 1) cells affine, kR x S1 packed at
     // e0 + kR*S1*i; the F cells of the blocks with an active camera packed in
     // block order from f0 (a constant camera has none; its block's first
-    // active entries are the E rows).  Per chunk of cse::kChunkC0 blocks:
-    // its first F cell, then the end of the F cells; and the first block
-    // with an active camera after the chunk (the lookahead lane).
+    // active entries are the E rows).  Per chunk of 64 blocks: its first F
+    // cell, then the end of the F cells.
     auto try_bsm = [&]() -> bool {
       const int64_t f0 = O[L[gidx(first[0])]];
       const int64_t e0 = O[L[gidx(0)] + (act(0) ? NR : 0)];
-      std::vector<int64_t> fb, lk;
+      std::vector<int64_t> fb;
       fb.reserve((size_t)nchunks + 1);
       int64_t rank = 0;
       for (int64_t i = 0; i < n; ++i) {
-        if (i % cse::kChunkC0 == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
+        if (i % cse::kWave == 0) fb.push_back(f0 + (int64_t)NR * S0 * rank);
         const int64_t base = L[gidx(i)];
         int a = 0;
         if (act(i)) {
@@ -969,23 +987,14 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
       G->jac_stride[0] = (int64_t)NR * S0;
       G->jac_stride[1] = (int64_t)NR * S1;
       fb.push_back(f0 + (int64_t)NR * S0 * rank);
-      lk.assign((size_t)nchunks, -1);
-      int64_t next_active = -1;
-      for (int64_t i = n - 1, c = nchunks - 1; c >= 0; --c) {
-        const int64_t lo = c * cse::kChunkC0;
-        lk[c] = next_active;
-        for (; i >= lo; --i)
-          if (act(i)) next_active = i;
-      }
       G->h_fbase = std::move(fb);
-      G->h_look = std::move(lk);
       return true;
     };
     // CompressedRowSparseMatrix (compressed_row_jacobian_writer.cc:145-185):
     // every block's rows packed in block order, NR x (S0 + S1) with an active
     // camera (camera and point at fixed columns of the row) and NR x S1 with
     // a held one (the point alone).  Per chunk: the offset of its first row,
-    // then the end; the lookahead lane takes the next chunk's first block.
+    // then the end.
     auto try_crs = [&]() -> bool {
       const int N = S0 + S1;
       const int64_t b0 = L[gidx(first[0])];
@@ -994,11 +1003,11 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
       const int camcol = (int)(cam0 - rb0), ptcol = (int)(pt0 - rb0);
       if (!((camcol == 0 && ptcol == S0) || (ptcol == 0 && camcol == S1))) return false;
       const int64_t r0 = rb0 - (int64_t)NR * S1 * first[0];
-      std::vector<int64_t> cb, lk;
+      std::vector<int64_t> cb;
       cb.reserve((size_t)nchunks + 1);
       int64_t pos = r0;
       for (int64_t i = 0; i < n; ++i) {
-        if (i % cse::kChunkC0 == 0) cb.push_back(pos);
+        if (i % cse::kWave == 0) cb.push_back(pos);
         const int64_t base = L[gidx(i)];
         if (act(i)) {
           for (int r = 0; r < NR; ++r)
@@ -1013,16 +1022,12 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
         }
       }
       cb.push_back(pos);
-      lk.assign((size_t)nchunks, -1);
-      for (int64_t c = 0; c < nchunks; ++c)
-        lk[c] = (c + 1) * cse::kChunkC0 < n ? (c + 1) * cse::kChunkC0 : -1;
       for (int r = 0; r < NR; ++r) {
         G->jac_base[0][r] = r0 + (int64_t)r * N + camcol;
         G->jac_base[1][r] = r0 + (int64_t)r * N + ptcol;
       }
       G->jac_stride[0] = G->jac_stride[1] = (int64_t)NR * N;
       G->h_fbase = std::move(cb);
-      G->h_look = std::move(lk);
       return true;
     };
     if (try_bsm()) return kAffinePacked;
@@ -1088,7 +1093,7 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.packed0_stride = G.packed_stride;
   a.act0_bits = G.act0.p;
   a.fbase = G.fbase.p;
-  a.look = G.look.p;
+  a.side = G.side.p;
   a.delta0 = G.delta0.p;
   a.gindex = G.gindex.p;
   a.first = G.first;
@@ -1127,7 +1132,7 @@ int FoldTiming(cse_evaluator* ev) {
 // add the slot-1 boundary entries and the slot-0 contributions, per
 // parameter block in a fixed order, into out (delta offsets).
 int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
-  const int64_t entries = 2 * ((G.n + G.chunk - 1) / G.chunk);
+  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
   hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
                      dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
@@ -1236,7 +1241,7 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
 // entries, then the slot-0 rows from the chunk sums, in a fixed order.
 int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s) {
   const Group::GradPlan& P = G.grad[0];
-  const int64_t entries = 2 * ((G.n + G.chunk - 1) / G.chunk);
+  const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
   hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
                      dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
@@ -1402,8 +1407,11 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     if (G.const0 && !fused) grad_pass = false;
     const bool recompute = fused && mode != 3;  // slot 0 by CameraGradientKernel
     cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
+    if (CSE_PERSISTENT != 0 && d_jac && d_res && !d_grad && G.policy == kAffinePacked && dma &&
+        !G.const0)
+      if (LaunchFn pf = PickPersistent(G.kind, G.loss.kind)) fn = pf;
     if (fused) {
-      const int64_t chunks = (G.n + G.chunk - 1) / G.chunk;
+      const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
       int rc;
       if ((rc = G.gside.ensure((size_t)(2 * chunks * 4)))) return rc;
       if (!recompute && (rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
@@ -1443,18 +1451,25 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
         }
       }
     }
-    if (G.const0) {
-      // The held-camera Jacobian kernels write ceil(n / kChunkC0) partials, the
-      // residual-only ones ceil(n / 64): after a switch to the smaller count
-      // the slots beyond it would keep the other kernel's values.
-      const int geometry = jets ? cse::kChunkC0 : cse::kWave;
-      if (geometry == cse::kWave && G.partials_chunk != cse::kWave)
-        CSE_HIP(hipMemsetAsync(ev->partials.p + G.partial_offset, 0,
-                               G.num_wg * cse::kWavesPerBlock * sizeof(double), ev->stream));
-      G.partials_chunk = geometry;
-    }
     fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
+    if (G.const0 && jets && d_jac && G.side.p) {
+      // The 64-byte sectors two held-camera chunks share (the full chunks
+      // stored their heads and tails in side slots), when the full chunks
+      // took that tail: the same base alignment test as the kernel.
+      const uintptr_t m = (d_res ? reinterpret_cast<uintptr_t>(d_res + G.res_base) : 0) |
+                          reinterpret_cast<uintptr_t>(d_jac + G.jac_base[1][0]) |
+                          reinterpret_cast<uintptr_t>(d_jac + G.h_fbase[0]);
+      if ((m & 15) == 0) {
+        const int64_t nchunks = (G.n + cse::kWave - 1) / cse::kWave;
+        const int64_t threads = 4 * nchunks;
+        hipLaunchKernelGGL(cse::HeldSectorFixupKernel,
+                           dim3((unsigned)((threads + cse::kBlockThreads - 1) / cse::kBlockThreads)),
+                           dim3(cse::kBlockThreads), 0, ev->stream, d_jac, G.fbase.p, G.side.p,
+                           G.prev_seg.p, nchunks, G.n / cse::kWave);
+        CSE_HIP(hipGetLastError());
+      }
+    }
     if (side && CSE_GRAD_CONCURRENT == 2) {  // queued behind the points kernel, low priority
       const int rc = LaunchCameraGradKernel(ev, G, d_state, ev->side, false);
       if (rc) return rc;
@@ -1701,8 +1716,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     if (G.const0) ev->any_general = true;
     if (!G.affine) ev->any_general = true;
     if (G.affine) {
-      G.chunk = G.const0 ? cse::kChunkC0 : cse::kWave;
-      const int64_t chunks = (g.num_blocks + G.chunk - 1) / G.chunk;
+      const int64_t chunks = (g.num_blocks + cse::kWave - 1) / cse::kWave;
       G.num_wg = std::max<int64_t>(1, (chunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock);
     } else {
       G.num_wg = (g.num_blocks + cse::kBlockThreads - 1) / cse::kBlockThreads;
@@ -1747,8 +1761,17 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       if ((rc = G.delta0.upload(dlt.data(), dlt.size(), s))) return bail(rc);
       if (!G.h_fbase.empty() && (rc = G.fbase.upload(G.h_fbase.data(), G.h_fbase.size(), s)))
         return bail(rc);
-      if (!G.h_look.empty() && (rc = G.look.upload(G.h_look.data(), G.h_look.size(), s)))
-        return bail(rc);
+      if (!G.h_fbase.empty()) {
+        const int64_t nchunks = (int64_t)G.h_fbase.size() - 1;
+        std::vector<int32_t> prev((size_t)nchunks, -1);
+        int32_t last = -1;
+        for (int64_t c = 0; c < nchunks; ++c) {
+          prev[c] = last;
+          if (G.h_fbase[c + 1] > G.h_fbase[c]) last = (int32_t)c;
+        }
+        if ((rc = G.prev_seg.upload(prev.data(), prev.size(), s))) return bail(rc);
+        if ((rc = G.side.alloc((size_t)nchunks * 16))) return bail(rc);
+      }
       if (hipStreamSynchronize(s) != hipSuccess) return bail(Fail(CSE_ERR_HIP, "upload failed"));
     }
     if (G.affine && ev->has_layout) {

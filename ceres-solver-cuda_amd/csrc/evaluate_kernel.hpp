@@ -41,15 +41,13 @@ namespace cse {
 //   kConst0 (BlockSparseMatrix): lanes with a constant slot-0 block (act0
 //       false) have no F cell; the others' cells are packed in lane order from
 //       fbase[c] (chunk c).
-//       head_skip: the full chunks before this one took the sector-aligned
-//       tail of the held-camera kernels, which wrote this chunk's F cells up
-//       to the first 64-byte boundary; those bytes are skipped.
+//       (Held-camera chunks staged here write their whole segment, head and
+//       tail included; HeldSectorFixupKernel leaves those bytes alone.)
 template <class K, bool kJac, bool kCrs, bool kHalves = false, bool kConst0 = false>
 __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, int lane, bool active,
                                               int64_t i0, int nw, const double* r,
                                               const double* J0, const double* J1,
-                                              bool act0 = true, int64_t c = 0,
-                                              bool head_skip = false) {
+                                              bool act0 = true, int64_t c = 0) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, NB = Tr::NB, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   constexpr int N = S0 + S1;
@@ -73,11 +71,7 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
       };
       const int ob = NR * S1 * below(m_any) + NR * S0 * below(m_act);
-      int skip = 0;
-      if (head_skip && c > 0) {
-        const uintptr_t A = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
-        skip = (int)((((A + 63) & ~(uintptr_t)63) - A) >> 3);
-      }
+      constexpr int skip = 0;
       if (active) {
         double* seg = a.jacobian + a.fbase[c];
         const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
@@ -146,14 +140,7 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
           for (int q = 0; q < NR * S0; ++q) st[rank * NR * S0 + q] = J0[q];
         }
         __builtin_amdgcn_wave_barrier();
-        const int cnt = __popcll(m) * NR * S0;
-        int skip = 0;
-        if (head_skip && c > 0) {
-          const uintptr_t A = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
-          skip = (int)((((A + 63) & ~(uintptr_t)63) - A) >> 3);
-          skip = skip < cnt ? skip : cnt;
-        }
-        WaveStore(st + skip, a.jacobian + a.fbase[c] + skip, cnt - skip, lane);
+        WaveStore(st, a.jacobian + a.fbase[c], __popcll(m) * NR * S0, lane);
       } else {
         if (active) {
 #pragma unroll
@@ -447,11 +434,13 @@ struct FusedGrad {
 
 // The points-only fused kernel writes the slot-1 copy for
 // CameraGradientKernel (GroupArgs::ppad): each point once per wave, by the
-// last lane of its run, from the values the wave loaded anyway (A/B builds:
-// -DCSE_POINT_COPY=0 leaves it out and the camera kernel gathers from the
-// state).
+// last lane of its run, from the values the wave loaded anyway.  Off
+// (CSE_POINT_COPY 0): measured neutral on problem-13682 (2.128 vs 2.133 ms
+// per gradient evaluation, profiles/round4/r4g/ab_grad) -- the camera
+// kernel's 24-byte point gathers already cost one sector request each, so a
+// sector-aligned copy saves no requests; -DCSE_POINT_COPY=1 builds it.
 #ifndef CSE_POINT_COPY
-#define CSE_POINT_COPY 1
+#define CSE_POINT_COPY 0
 #endif
 
 // Can the wave take the back-to-back store tail?  Full chunk, 16-byte
@@ -697,14 +686,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
   __shared__ double stage[kWPB][kWave * kStageLane];
 
-  // Held-camera groups: kChunkC0 blocks a wave, lane kChunkC0 evaluating the
-  // first block with an active camera after the chunk (its F cell's head
-  // completes this wave's last 64-byte sector).
   constexpr bool kC0J = T::kConst0 && kJac;
-  constexpr int kChunk = kC0J ? kChunkC0 : kWave;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
-  const int64_t num_chunks = (a.n + kChunk - 1) / kChunk;
+  const int64_t num_chunks = (a.n + kWave - 1) / kWave;
   const int64_t wg = T::kXcdMap ? XcdContiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t c = wg * kWPB + wave;
   double* partial_dst = a.partials + c;
@@ -713,14 +698,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     return;
   }
   double* st = stage[wave];
-  const int64_t i0 = c * kChunk;
+  const int64_t i0 = c * kWave;
   const int64_t rem = a.n - i0;
-  const int nw = rem < kChunk ? (int)rem : kChunk;
+  const int nw = rem < kWave ? (int)rem : kWave;
   const bool active = lane < nw;
-  int64_t look_i = -1;
-  if constexpr (kC0J) look_i = nw == kChunk ? a.look[c] : -1;
-  const bool look = kC0J && lane == kChunk && look_i >= 0;
-  const int64_t i = active ? i0 + lane : (look ? look_i : a.n - 1);
+  const int64_t i = active ? i0 + lane : a.n - 1;
 
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(2);
   AffineInputs<K> in;
@@ -809,45 +791,52 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
   if constexpr (kC0J) {
-    if (nw == kChunk && C0Aligned(a)) {
-      // ---- held-camera groups, full chunk: sector-aligned windows ----
-      // F: this wave writes [W0, W1): from its first F cell rounded up to a
-      // 64-byte sector (the previous wave wrote the head) to the next chunk's
-      // first F cell rounded up (its head comes from the lookahead lane), so
-      // every store covers whole sectors wherever held blocks shifted the
-      // packed cells; E (48 B) and residuals (16 B) of 60 blocks are whole
-      // sectors by themselves.
+    if (nw == kWave && C0Aligned(a)) {
+      // ---- held-camera groups, full chunk: whole-sector windows ----
+      // After a held block the packed F cells (BSM) or row blocks (CRS) no
+      // longer start on 64-byte sectors.  The wave stores only the whole
+      // sectors of its segment, [W0, W1) = [A0 rounded up, A1 rounded down),
+      // and its head and tail pieces (up to three of 16 B each) into its two
+      // 64-byte side slots, one store; HeldSectorFixupKernel then writes each
+      // sector shared by two waves in one piece.  The group's first and last
+      // non-empty segments write their outer ends directly.
       static_assert(NR == 2 && S1 > 0, "held-camera tail: two-slot kinds, two residuals");
-      constexpr int kF = NR * S0;  // doubles per F cell (BSM); a row block's camera part (CRS)
-      // BlockSparseMatrix: the F window (up to 60 cells and the head of the
-      // next), then the E cells.  CompressedRowSparseMatrix: one window over
-      // the chunk's row blocks (NR x (S1 + S0) with an active camera, NR x S1
-      // with a held one), staged in two halves of the wave.
-      constexpr int kSegPieces = kCrs ? kChunkC0 * NR * (S0 + S1) / 2 : kChunkC0 * kF / 2;
-      constexpr int kQF = (kSegPieces + 3 + kWave - 1) / kWave;
-      constexpr int kPE = kCrs ? 0 : kChunkC0 * NR * S1 / 2;  // E pieces of a chunk (BSM)
+      constexpr int kF = NR * S0;  // doubles per F cell (BSM)
+      // BlockSparseMatrix: the F window, then the E cells.  CompressedRow:
+      // one window over the chunk's row blocks (NR x (S1 + S0) with an active
+      // camera, NR x S1 with a held one), staged in two halves of the wave.
+      constexpr int kSegPieces = kCrs ? kWave * NR * (S0 + S1) / 2 : kWave * kF / 2;
+      constexpr int kQF = (kSegPieces + kWave - 1) / kWave;
+      constexpr int kPE = kCrs ? 0 : kWave * NR * S1 / 2;  // E pieces of a chunk (BSM)
       constexpr int kQE = kCrs ? 1 : (kPE + kWave - 1) / kWave;
       constexpr int kLdsPieces = kWave * kStageLane / 2;
-      static_assert(kChunkC0 % 4 == 0 && kQF <= 16, "window: one or two base registers");
+      static_assert(kQF <= 16, "window: one or two base registers");
       const bool jacw = a.jacobian != nullptr;
-      cse_v4i qf[kQF], qe[kQE];
+      cse_v4i qf[kQF], qe[kQE], qs;
       double* wf0 = nullptr;
       double* wf1 = nullptr;
       double* we0 = nullptr;
+      double* ws = nullptr;
       int P = 0;
       if (jacw) {
-        const uintptr_t A0 = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c]);
-        const uintptr_t A1 = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[c + 1]);
-        const uintptr_t AE = reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[num_chunks]);
-        const uintptr_t W0 = c == 0 ? A0 : ((A0 + 63) & ~(uintptr_t)63);
-        const uintptr_t W1 = A1 == AE ? A1 : ((A1 + 63) & ~(uintptr_t)63);
+        const int64_t fb0 = a.fbase[c], fb1 = a.fbase[c + 1];
+        const uintptr_t A0 = reinterpret_cast<uintptr_t>(a.jacobian + fb0);
+        const uintptr_t A1 = reinterpret_cast<uintptr_t>(a.jacobian + fb1);
+        const bool first = fb0 == a.fbase[0], last = fb1 == a.fbase[num_chunks];
+        const uintptr_t W0 = first ? A0 : ((A0 + 63) & ~(uintptr_t)63);
+        const uintptr_t W1 = last ? A1 : (A1 & ~(uintptr_t)63);
         P = W1 > W0 ? (int)((W1 - W0) >> 4) : 0;
-        const int off = W1 > W0 ? (int)((W0 - A0) >> 4) : 0;
+        const int off = (int)((W0 - A0) >> 4);            // head pieces (not stored here)
+        const int npc = (int)((A1 - A0) >> 4);            // pieces of the segment
+        const int tp = W1 > W0 ? (int)((A1 - W1) >> 4) : 0;  // tail pieces
+        // Side slots: lanes 0-3 the head sector's pieces at their positions
+        // (the head is its last `off` pieces), lanes 4-7 the tail sector's.
+        int sp = lane < 4 ? lane - (4 - off) : npc - tp + (lane - 4);
+        sp = sp < 0 ? 0 : (sp < npc ? sp : (npc > 0 ? npc - 1 : 0));
         const double2* st2 = reinterpret_cast<const double2*>(st);
         if constexpr (kCrs) {
           constexpr int N = S0 + S1;
-          const bool out = active || look;
-          const uint64_t m_any = __ballot(out), m_act = __ballot(out && act0);
+          const uint64_t m_any = __ballot(active), m_act = __ballot(active && act0);
           auto below = [&](uint64_t mm) {
             return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
@@ -856,13 +845,13 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
           const int ob = NR * S1 * below(m_any) + NR * S0 * below(m_act);
           const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
           const int camcol = (int)(a.jac_base[0][0] - row0), ptcol = (int)(a.jac_base[1][0] - row0);
-          constexpr int kHalf = kChunkC0 / 2;
+          constexpr int kHalf = kWave / 2;
           const int split = __builtin_amdgcn_readlane(ob, kHalf);  // where lane kHalf's block starts
-          const int total = __builtin_amdgcn_readlane(ob, kWave - 1);
+          const int total = 2 * npc;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int lo = h == 0 ? 0 : split, hi = h == 0 ? split : total;
-            if (out && (h == 0 ? lane < kHalf : lane >= kHalf)) {
+            if (active && (h == 0 ? lane < kHalf : lane >= kHalf)) {
               double* blk = st + (ob - lo);
               if (act0) {
 #pragma unroll
@@ -890,14 +879,20 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
                 qf[j] = AsV4i(v.x, v.y);
               }
             }
+            if (2 * sp >= lo && 2 * sp < hi) {
+              int p = sp - (lo >> 1);
+              p = p < kLdsPieces ? p : kLdsPieces - 1;
+              const double2 v = st2[p];
+              qs = AsV4i(v.x, v.y);
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
           }
         } else {
-          const uint64_t m = __ballot((active || look) && act0);
+          const uint64_t m = __ballot(active && act0);
           const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          if ((active || look) && act0) {
+          if (active && act0) {
 #pragma unroll
             for (int q = 0; q < kF; ++q) st[rank * kF + q] = J0[q];
           }
@@ -908,6 +903,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
             p = p < kLdsPieces ? p : kLdsPieces - 1;
             const double2 v = st2[p];
             qf[j] = AsV4i(v.x, v.y);
+          }
+          {
+            const double2 v = st2[sp < kLdsPieces ? sp : kLdsPieces - 1];
+            qs = AsV4i(v.x, v.y);
           }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
@@ -930,6 +929,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         double* fw = reinterpret_cast<double*>(W0);
         wf0 = fw + 2 * lane + 512;
         wf1 = fw + 2 * lane + 1536;
+        ws = a.side + 16 * c + 2 * lane;
       }
       const cse_v4i qr = AsV4i(r[0], r[1]);
       double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;
@@ -941,7 +941,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       // blocks (10 doubles each, block order), staged like the cells.
       constexpr bool kContribC0 = kGradF && !T::kNoContrib;
       constexpr int kGQ = kContribC0 ? FusedGrad<K>::S0p / 2 : 1;  // pieces per block
-      constexpr int kPC = kChunkC0 * kGQ;
+      constexpr int kPC = kWave * kGQ;
       constexpr int kQC = kContribC0 ? (kPC + kWave - 1) / kWave : 1;
       cse_v4i qc[kQC];
       double* cb0 = nullptr;
@@ -978,10 +978,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       double* v_partial = partial_dst;
       double v_wsum = wsum;
       asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
-      asm volatile("" ::"v"(wf0), "v"(wf1), "v"(we0), "v"(rdst));
+      asm volatile("" ::"v"(wf0), "v"(wf1), "v"(we0), "v"(ws), "v"(rdst));
       // ---- every store of the wave ----
       if (jacw) {
         SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
+        if (lane < 8) StoreNt16<0, 1>(ws, qs);
         if constexpr (!kCrs) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
       }
       if (a.residuals && active) StoreNt16<0>(rdst, qr);
@@ -1013,7 +1014,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       }
       KeepAlive<kQF>(qf);
       KeepAlive<kQE>(qe);
-      asm volatile("" ::"v"(qr), "v"(wf0), "v"(wf1), "v"(we0), "v"(rdst), "v"(v_partial), "v"(v_wsum));
+      asm volatile("" ::"v"(qr), "v"(qs), "v"(ws), "v"(wf0), "v"(wf1), "v"(we0), "v"(rdst),
+                   "v"(v_partial), "v"(v_wsum));
       if constexpr (kGradF) {
         KeepAlive<2>(sq);
         asm volatile("" ::"v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
@@ -1028,10 +1030,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   bool fast = FastTail<K, kJac, kCrs, T::kConst0>(a, i0, nw, c);
   if constexpr (kC0J) fast = false;  // full aligned chunks returned above
   if (!fast) {
-    bool head_skip = false;
-    if constexpr (kC0J) head_skip = C0Aligned(a);
-    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c,
-                                                       head_skip);
+    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;

@@ -19,11 +19,7 @@ constexpr int kBlockThreads = 256;
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = kBlockThreads / kWave;
 constexpr int kMaxSlots = 10;  // parameter blocks per residual block (table path)
-// Blocks per wave of the affine Jacobian kernels for groups with constant
-// slot-0 blocks (held cameras): 60 (a multiple of 4, so the E cells and
-// residuals of every wave start on a 64-byte sector), lane 60 evaluating the
-// next wave's first F cell ahead (EvaluateAffineChunks* with Tune::kConst0).
-constexpr int kChunkC0 = 60;
+
 
 // kImpossibleValue (internal/ceres/array_utils.h:52): the marker
 // AutoDifferentiate pre-fills outputs with.
@@ -65,8 +61,11 @@ struct GroupArgs {
   // (id - packed0_lo) of act0_bits set = active; the F cells of the active
   // blocks of chunk c start at fbase[c] (no cell for a constant block).
   const uint32_t* act0_bits;
-  const int64_t* fbase;   // [chunks + 1] (kChunkC0-block chunks), the last = end of the F cells
-  const int64_t* look;    // [chunks] the first block with an active slot 0 after chunk c, or -1
+  const int64_t* fbase;   // [chunks + 1] (64-block chunks), the last = end of the F cells
+  // [chunks][16]: each full chunk's head and tail pieces of its F segment
+  // (BSM) or row-block segment (CRS), in two 64-byte slots, for
+  // HeldSectorFixupKernel.
+  double* side;
   const int64_t* delta0;  // [slot-0 id - packed0_lo] delta offset of an active block
   // Table policy.
   const int64_t* gindex;

@@ -562,6 +562,44 @@ __global__ __launch_bounds__(kBlockThreads) void QuaternionPlusKernel(const doub
   for (int k = 4; k < B.size; ++k) o[k] = q[k] + d[k - 1];
 }
 
+// Held-camera groups (Tune::kConst0 Jacobian kernels): after a held block
+// the packed F cells (BSM) or row blocks (CRS) of a chunk start inside a
+// 64-byte sector.  Each full chunk stored only the whole sectors of its
+// segment and put its head pieces (slots 0-3: at their positions in the
+// sector before its first whole one) and its tail pieces (slots 4-7: at their
+// positions in the sector after its last) into side[16 c ..]; here thread
+// 4 c + pos assembles position pos of the sector chunk c shares with the
+// previous chunk that has a segment (prev[c]): the tail of that chunk, then
+// the head of c, each only if that chunk was full (c < nfull; a ragged last
+// chunk writes its whole segment itself), so each such sector is written as
+// one 64-byte piece instead of two partial writes.  The group's first
+// segment wrote its head itself.
+__global__ __launch_bounds__(kBlockThreads) void HeldSectorFixupKernel(double* jac, const int64_t* fbase,
+                                                                       const double* side,
+                                                                       const int32_t* prev,
+                                                                       int64_t nchunks, int64_t nfull) {
+  const int64_t t = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  const int64_t c = t >> 2;
+  const int pos = (int)(t & 3);
+  if (c >= nchunks || c == 0) return;
+  const int64_t f0 = fbase[c];
+  if (fbase[c + 1] == f0 || f0 == fbase[0]) return;  // no segment, or the first one
+  const uintptr_t A0 = reinterpret_cast<uintptr_t>(jac + f0);
+  const int hp = (int)(((64 - (A0 & 63)) & 63) >> 4);  // head pieces of c
+  if (hp == 0) return;                                    // starts on a sector
+  const int64_t pc = prev[c];
+  const double* src = nullptr;
+  if (pos < 4 - hp) {
+    if (pc >= 0 && pc < nfull) src = side + 16 * pc + 8 + 2 * pos;
+  } else if (c < nfull) {
+    src = side + 16 * c + 2 * pos;
+  }
+  if (src) {
+    double* S = reinterpret_cast<double*>(A0 & ~(uintptr_t)63);
+    *reinterpret_cast<double2*>(S + 2 * pos) = *reinterpret_cast<const double2*>(src);
+  }
+}
+
 // Sums the per-workgroup partials of every group in a fixed order, writes
 // the cost, publishes the evaluation status and re-arms the status word
 // for the next evaluation (replaces thrust::reduce + the abort-flag round

@@ -6,9 +6,10 @@ of that camera have no F cell, so every later block's F cell moves up by one
 cell (block_jacobian_writer.cc:75-149), and the camera's values come from the
 constant state (registered_cuda_evaluators.cc:237-248).  Groups whose slot-0
 blocks are partly constant stay on the affine kernels (cse::ShippedTuneC0:
-F cells packed in block order from a per-chunk base, 60-block waves whose
-stores cover whole 64-byte sectors); the same for CompressedRowSparseMatrix,
-whose row blocks then have two widths.  Against the oracle
+F cells packed in block order from a per-chunk base, every store a whole
+64-byte sector, the sectors two waves share written by HeldSectorFixupKernel);
+the same for CompressedRowSparseMatrix, whose row blocks then have two
+widths.  Against the oracle
 (tests/parity_util.py tolerances): both layouts, losses, the four gradient modes, residual/cost-only,
 ragged sizes, whole chunks of held cameras, the quaternion manifold, the
 Jacobian products and the multi-device evaluator; the reference's own mix is
@@ -100,19 +101,22 @@ def test_held_cameras_ragged(gpu, n_obs):
 
 
 @pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
-@pytest.mark.parametrize("n_obs", [600, 601, 658, 1200])
+@pytest.mark.parametrize("n_obs", [600, 601, 658, 1200, 2003])
 @pytest.mark.parametrize("mode", [0, 3])
 def test_held_blocks_at_chunk_boundaries(gpu, n_obs, mode, fmt):
-    """The held-camera kernels cut the blocks into waves of 60 (cse::kChunkC0)
-    and each wave writes its F cells up to the next 64-byte sector, taking the
-    head of the next wave's first F cell from a lookahead lane.  Held blocks
-    right at and around the cuts (the lookahead then skips them), four in a
-    row, a wave whose cells start mid-sector, ragged ends: against the oracle
-    and bit-identical to the table path (residuals, Jacobian)."""
+    """A held block shifts every later F cell (BSM) or row block (CRS) by a
+    quarter sector, so a wave's segment starts and ends inside 64-byte
+    sectors: full waves store their whole sectors and put their head and tail
+    pieces into side slots, and HeldSectorFixupKernel writes each shared
+    sector.  Held blocks at and around the 64-block cuts, four in a row (the
+    shift back to aligned), a whole wave of held blocks (an empty segment
+    between two others), ragged ends: against the oracle and bit-identical to
+    the table path (residuals, Jacobian)."""
     rng = np.random.default_rng(n_obs + mode)
     C, P = 8, n_obs // 3
-    held_blocks = {0, 59, 60, 61, 119, 120, 179, 180, 181, 182, 183, 239, 299, 300, 301, 302,
-                   359, 420, 540, 541, 599, 600, 601, 659, 660, 1139, 1140, 1199}
+    held_blocks = {0, 63, 64, 65, 127, 128, 191, 192, 193, 194, 195, 255, 319, 320, 321, 322,
+                   383, 448, 575, 576, 599, 600, 601, 639, 640, 1087, 1088, 1151, 1199}
+    held_blocks |= set(range(704, 768))  # chunk 11: no F cell at all
     ci = rng.integers(1, C, n_obs)
     for b in held_blocks:
         if b < n_obs:

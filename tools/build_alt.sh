@@ -9,4 +9,8 @@ mkdir -p build/$NAME lib/$NAME
 make -s build/layout.o build/multi_device.o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-signed-zeros -ffinite-math-only \
   -munsafe-fp-atomics -Wall -Wno-unused-function "$@" -c -o build/$NAME/cse_evaluator.o csrc/cse_evaluator.hip
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/$NAME/libcse.so build/$NAME/cse_evaluator.o build/multi_device.o build/layout.o
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-signed-zeros -ffinite-math-only \
+  -munsafe-fp-atomics -Wall -Wno-unused-function -mllvm -disable-machine-licm "$@" \
+  -c -o build/$NAME/persistent.o csrc/persistent.hip
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/$NAME/libcse.so build/$NAME/cse_evaluator.o \
+  build/$NAME/persistent.o build/multi_device.o build/layout.o
