@@ -533,12 +533,13 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
 // Held-camera groups (Tune::kConst0): may full chunks take the sector-aligned
 // tail?  The residual, E-cell and F-cell bases 16-byte aligned (the chunk
 // segments then start on 64-byte sectors when the bases do).
-__device__ __forceinline__ bool C0Aligned(const GroupArgs& a) {
+// fb_first: a.fbase[0].
+__device__ __forceinline__ bool C0Aligned(const GroupArgs& a, int64_t fb_first) {
   uintptr_t m = 0;
   if (a.residuals) m |= reinterpret_cast<uintptr_t>(a.residuals + a.res_base);
   if (a.jacobian)
     m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[1][0]) |
-         reinterpret_cast<uintptr_t>(a.jacobian + a.fbase[0]);
+         reinterpret_cast<uintptr_t>(a.jacobian + fb_first);
   return (m & 15) == 0;
 }
 
@@ -703,6 +704,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int nw = rem < kWave ? (int)rem : kWave;
   const bool active = lane < nw;
   const int64_t i = active ? i0 + lane : a.n - 1;
+  // Held-camera groups: the chunk's packed-F bounds and the group's, loaded
+  // here, before the gather's memory-clobbering asm, so that the scalar
+  // loads' latency is not in the store tail.
+  int64_t fb[4] = {0, 0, 0, 0};
+  if constexpr (kC0J) {
+    if (a.jacobian != nullptr) {
+      fb[0] = a.fbase[c];
+      fb[1] = a.fbase[c + 1];
+      fb[2] = a.fbase[0];
+      fb[3] = a.fbase[num_chunks];
+    }
+  }
 
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(2);
   AffineInputs<K> in;
@@ -791,7 +804,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
   if constexpr (kC0J) {
-    if (nw == kWave && C0Aligned(a)) {
+    if (nw == kWave && C0Aligned(a, fb[2])) {
       // ---- held-camera groups, full chunk: whole-sector windows ----
       // After a held block the packed F cells (BSM) or row blocks (CRS) no
       // longer start on 64-byte sectors.  The wave stores only the whole
@@ -819,10 +832,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       double* ws = nullptr;
       int P = 0;
       if (jacw) {
-        const int64_t fb0 = a.fbase[c], fb1 = a.fbase[c + 1];
+        const int64_t fb0 = fb[0], fb1 = fb[1];
         const uintptr_t A0 = reinterpret_cast<uintptr_t>(a.jacobian + fb0);
         const uintptr_t A1 = reinterpret_cast<uintptr_t>(a.jacobian + fb1);
-        const bool first = fb0 == a.fbase[0], last = fb1 == a.fbase[num_chunks];
+        const bool first = fb0 == fb[2], last = fb1 == fb[3];
         const uintptr_t W0 = first ? A0 : ((A0 + 63) & ~(uintptr_t)63);
         const uintptr_t W1 = last ? A1 : (A1 & ~(uintptr_t)63);
         P = W1 > W0 ? (int)((W1 - W0) >> 4) : 0;
