@@ -244,9 +244,7 @@ constexpr int kOperatorWavesPerWg = CSE_OPERATOR_W1 ? 1 : cse::kWavesPerBlock;
 // workgroups sum slices and the last of them finalises
 // (ReduceFinalizeKernel); below, one FinalizeKernel.
 constexpr int64_t kPartialsTwoPass = 4096;
-// 1024 slices: each workgroup's threads load one or two partials (the
-// 128-slice form took 11 us at problem-13682, latency-bound).
-constexpr int kPartialBlocks = cse::kFinalizeSlices;
+constexpr int kPartialBlocks = 128;
 
 // Layout policy of a group: 0 = table, 1 = affine packed cells (BSM),
 // 2 = affine interleaved rows (CRS).

@@ -439,6 +439,12 @@ struct FusedGrad {
 // per gradient evaluation, profiles/round4/r4g/ab_grad) -- the camera
 // kernel's 24-byte point gathers already cost one sector request each, so a
 // sector-aligned copy saves no requests; -DCSE_POINT_COPY=1 builds it.
+// Held-camera tail variants for A/B builds (0: shipped; 1: chunks without
+// a held block take the usual tail from fbase[c], partial sectors and all).
+#ifndef CSE_C0_VARIANT
+#define CSE_C0_VARIANT 0
+#endif
+
 #ifndef CSE_POINT_COPY
 #define CSE_POINT_COPY 0
 #endif
@@ -706,15 +712,14 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int64_t i = active ? i0 + lane : a.n - 1;
   // Held-camera groups: the chunk's packed-F bounds and the group's, loaded
   // here, before the gather's memory-clobbering asm, so that the scalar
-  // loads' latency is not in the store tail.
-  int64_t fb[4] = {0, 0, 0, 0};
-  if constexpr (kC0J) {
-    if (a.jacobian != nullptr) {
-      fb[0] = a.fbase[c];
-      fb[1] = a.fbase[c + 1];
-      fb[2] = a.fbase[0];
-      fb[3] = a.fbase[num_chunks];
-    }
+  // loads' latency is in neither the gather nor the store tail.
+  int64_t fb[5] = {0, 0, 0, 0, 0};
+  if constexpr (kC0J) {  // fbase is set for every held-camera group
+    fb[0] = a.fbase[c];
+    fb[1] = a.fbase[c + 1];
+    fb[2] = a.fbase[0];
+    fb[3] = a.fbase[num_chunks];
+    fb[4] = a.fbase[c + 2 < num_chunks ? c + 2 : num_chunks];
   }
 
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(2);
@@ -750,6 +755,15 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     GatherCoop<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
   }
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(0);
+  // The chunk bounds' first use, after the gather: their scalar loads were
+  // issued before it and have long arrived (without the pin the compiler
+  // compares them right away and waits for them before the gather starts).
+  if constexpr (kC0J) {
+    if constexpr (kWPB == 1)  // uniform: SGPRs
+      asm volatile("" : "+s"(fb[0]), "+s"(fb[1]), "+s"(fb[2]), "+s"(fb[3]), "+s"(fb[4]));
+    else  // the wave index is not known uniform to the compiler
+      asm volatile("" : "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]), "+v"(fb[4]));
+  }
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok;
 #ifdef CSE_TUNING
@@ -804,7 +818,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
   if constexpr (kC0J) {
-    if (nw == kWave && C0Aligned(a, fb[2])) {
+    // A/B builds only: CSE_C0_VARIANT 1 sends full chunks without a held
+    // block to the usual tail (seg0 = fbase[c], any 16-byte alignment).
+    bool c0_tail = nw == kWave && C0Aligned(a, fb[2]);
+    if (CSE_C0_VARIANT == 1 && __ballot(act0 || !active) == ~0ull) c0_tail = false;
+    if (c0_tail) {
       // ---- held-camera groups, full chunk: whole-sector windows ----
       // After a held block the packed F cells (BSM) or row blocks (CRS) no
       // longer start on 64-byte sectors.  The wave stores only the whole
@@ -831,6 +849,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       double* we0 = nullptr;
       double* ws = nullptr;
       int P = 0;
+      bool whole = false;  // every F store unmasked (below)
       if (jacw) {
         const int64_t fb0 = fb[0], fb1 = fb[1];
         const uintptr_t A0 = reinterpret_cast<uintptr_t>(a.jacobian + fb0);
@@ -842,6 +861,14 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         const int off = (int)((W0 - A0) >> 4);            // head pieces (not stored here)
         const int npc = (int)((A1 - A0) >> 4);            // pieces of the segment
         const int tp = W1 > W0 ? (int)((A1 - W1) >> 4) : 0;  // tail pieces
+        // A chunk without held blocks (npc = the whole staged segment) whose
+        // next chunk is full and has F cells: its window's store
+        // instructions run unmasked.  The lanes past the window then write
+        // the tail pieces and, past A1, the next segment's head pieces in
+        // the one sector the two share (P >= kQF * 64 - 4 here), which
+        // HeldSectorFixupKernel rewrites whole after this kernel.  Masked
+        // (exec-branched) stores made the held-camera kernel 15 % slower.
+        whole = npc == kQF * kWave && !last && (c + 2) * kWave <= a.n && fb[4] > fb1;
         // Side slots: lanes 0-3 the head sector's pieces at their positions
         // (the head is its last `off` pieces), lanes 4-7 the tail sector's.
         int sp = lane < 4 ? lane - (4 - off) : npc - tp + (lane - 4);
@@ -994,7 +1021,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       asm volatile("" ::"v"(wf0), "v"(wf1), "v"(we0), "v"(ws), "v"(rdst));
       // ---- every store of the wave ----
       if (jacw) {
-        SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
+        if (whole)
+          SegmentStoresMasked<0, kQF>(wf0, wf1, qf, 0, kQF * kWave);  // no lane masked
+        else
+          SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
         if (lane < 8) StoreNt16<0, 1>(ws, qs);
         if constexpr (!kCrs) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
       }
@@ -1041,7 +1071,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     }
   }
   bool fast = FastTail<K, kJac, kCrs, T::kConst0>(a, i0, nw, c);
-  if constexpr (kC0J) fast = false;  // full aligned chunks returned above
+  if constexpr (kC0J)  // full aligned chunks returned above
+    fast = CSE_C0_VARIANT == 1 && fast && __ballot(act0 || !active) == ~0ull;
   if (!fast) {
     StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
     if constexpr (kGradF) {

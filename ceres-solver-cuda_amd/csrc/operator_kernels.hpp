@@ -634,18 +634,16 @@ __global__ __launch_bounds__(1024) void FinalizeKernel(const double* partials, i
   }
 }
 
-// Many partials, one launch: workgroup b (of at most kFinalizeSlices) sums
-// partials [b*per, (b+1)*per)
+// Many partials, one launch: workgroup b sums partials [b*per, (b+1)*per)
 // in a fixed order and hands its sum over to
 // whichever workgroup finishes last, which adds the G slice sums in slice
 // order and finalises as FinalizeKernel does -- the same value, bit for bit,
-// as a slice pass followed by a fixed-order sum of the slice sums.  Hand-over (MI355X_MICROARCH.md, valid
+// as a slice pass followed by FinalizeKernel over the 128 slice sums.  Hand-over (MI355X_MICROARCH.md, valid
 // forms: one lane per storing workgroup, agent-scope atomic add, the last
 // adder told by the returned value): the slice sum is stored write-through
 // (sc1) and drained (vmcnt(0)) before the add; the last workgroup reads the
 // sums with sc1 loads only after its add has returned.  The counter is left
 // at 0 for the next launch.
-constexpr int kFinalizeSlices = 1024;
 __global__ __launch_bounds__(kBlockThreads) void ReduceFinalizeKernel(
     const double* partials, int64_t n, int64_t per, double* slices, int* counter, double* cost,
     int* status, int* status_out) {
@@ -665,22 +663,12 @@ __global__ __launch_bounds__(kBlockThreads) void ReduceFinalizeKernel(
   }
   __syncthreads();
   if (!last) return;
-  // Thread t adds slices t, t + 256, ... in that order (all loads issued
-  // before the one wait).
-  static_assert(kFinalizeSlices % kBlockThreads == 0, "whole rounds of slices");
-  constexpr int kRounds = kFinalizeSlices / kBlockThreads;
-  double sv[kRounds];
-#pragma unroll
-  for (int j = 0; j < kRounds; ++j) {
-    const unsigned k = threadIdx.x + j * kBlockThreads;
-    const double* src = slices + (k < gridDim.x ? k : 0);
-    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(sv[j]) : "v"(src) : "memory");
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   double s = 0.0;
-#pragma unroll
-  for (int j = 0; j < kRounds; ++j)
-    if (threadIdx.x + j * kBlockThreads < gridDim.x) s += sv[j];
+  if (threadIdx.x < gridDim.x) {
+    const double* src = slices + threadIdx.x;
+    asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(s) : "v"(src)
+                 : "memory");
+  }
   __syncthreads();  // lds_sum is reused
   const double total = WorkgroupSum(s, lds_sum);
   if (threadIdx.x == 0) {

@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
     ap.add_argument("--held-cameras", type=int, default=0,
                     help="hold the first K cameras constant (the const0 kernels)")
+    ap.add_argument("--held-tail", type=int, default=0,
+                    help="append one held camera observed by the last K blocks only (the "
+                         "held-camera kernels on an otherwise aligned layout)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="time rank 0's shard of an N-way point-bucket cut instead")
     args = ap.parse_args()
@@ -58,6 +61,13 @@ def main():
         from ceres_amd import shard
         prog = shard.shard_program(*bal.synthetic(*bal.CONFIGS[args.config]), 0, args.shard_of,
                                    loss=loss, format=args.format)[0]
+    elif args.held_tail > 0:
+        cams, pts, ci, pi, obs = bal.synthetic(*bal.CONFIGS[args.config])
+        cams = np.vstack([cams, cams[:1]])
+        ci = np.array(ci, copy=True)
+        ci[-args.held_tail:] = len(cams) - 1
+        prog = bal.program(cams, pts, ci, pi, obs, loss=loss, format=args.format,
+                           constant_cameras=(len(cams) - 1,))
     else:
         prog = bal.synthetic_program(args.config, loss=loss, format=args.format,
                                      constant_cameras=tuple(range(args.held_cameras)))
