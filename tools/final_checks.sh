@@ -3,7 +3,7 @@
 # default bench line, and a rocprofv3 kernel-trace summary of the same bench.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export CSE_BAL_CACHE=/tmp/cse_bal_cache
-OUT=gpurun_out/final
+OUT=gpurun_out/${TAG:-final}
 mkdir -p $OUT
 set -o pipefail
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --durations=15 --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || { echo "pytest rc=$?"; tail -20 $OUT/pytest_gpu.txt; exit 1; }

@@ -3,7 +3,7 @@
 # gradient (run under gpurun from the repo root).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export CSE_BAL_CACHE=/tmp/cse_bal_cache
-OUT=gpurun_out/configs.txt
+OUT=gpurun_out/${TAG:-configs}.txt
 : > $OUT
 while read -r args; do
   [ -z "$args" ] && continue
