@@ -142,12 +142,23 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
         __builtin_amdgcn_wave_barrier();
         WaveStore(st, a.jacobian + a.fbase[c], __popcll(m) * NR * S0, lane);
       } else {
-        if (active) {
+        constexpr int kParts = kHalves ? 2 : 1, kLanes = kWave / kParts;
 #pragma unroll
-          for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
+        for (int h = 0; h < kParts; ++h) {
+          const int lo = h * kLanes;
+          const int cnt = nw - lo < kLanes ? nw - lo : kLanes;
+          if (cnt <= 0) break;
+          if (h > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+          }
+          if (active && lane >= lo && lane < lo + kLanes) {
+#pragma unroll
+            for (int q = 0; q < NR * S0; ++q) st[(lane - lo) * NR * S0 + q] = J0[q];
+          }
+          __builtin_amdgcn_wave_barrier();
+          WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * (i0 + lo), cnt * NR * S0, lane);
         }
-        __builtin_amdgcn_wave_barrier();
-        WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
       }
       if constexpr (S1 > 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -439,6 +450,12 @@ struct FusedGrad {
 // per gradient evaluation, profiles/round4/r4g/ab_grad) -- the camera
 // kernel's 24-byte point gathers already cost one sector request each, so a
 // sector-aligned copy saves no requests; -DCSE_POINT_COPY=1 builds it.
+// BlockSparseMatrix F cells staged for lanes [0, 32), then [32, 64), through
+// half the LDS (1), or for the whole wave at once (0).
+#ifndef CSE_F_HALVES
+#define CSE_F_HALVES 0
+#endif
+
 // Held-camera tail variants for A/B builds (0: shipped; 1: chunks without
 // a held block take the usual tail from fbase[c], partial sectors and all).
 #ifndef CSE_C0_VARIANT
@@ -680,15 +697,23 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   // CRS rows staged in two halves of the wave (lanes [0, 32), then [32, 64)).
   constexpr bool kTwoCrs = T::kTwoRound && kJac && kCrs;
   constexpr int kA = T::kAlign;
+  // BSM F cells in two half-wave rounds (CSE_F_HALVES; not the held-camera
+  // kernels, which stage compacted cells).
+  constexpr bool kHalfF = CSE_F_HALVES != 0 && kTwo && !T::kConst0 && (NR * S0) % 2 == 0;
   constexpr int kOutLane = kJac ? (kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N)
+                                        : kHalfF ? (NR * S0 / 2 > NR * S1 ? NR * S0 / 2 : NR * S1)
                                         : kTwo ? NR * (S0 > S1 ? S0 : S1)
                                                : kLdsE ? NR * (S0 + S1) : NR * S0)
                                 : 1;
   constexpr int kCoopLane = kCoop == 2 ? ((Tr::X0 + 1) & ~1) : Tr::X0;
   // StageAndStore's footprint (ragged chunks): whole rows (CRS) or one
   // slot's cells at a time (BSM).
-  constexpr int kSlowLane = !kJac ? 1 : kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N) : NR * (S0 > S1 ? S0 : S1);
-  constexpr int kStageLane0 = kCoopLane > kOutLane ? kCoopLane : kOutLane;
+  constexpr int kSlowLane = !kJac ? 1 : kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N)
+                                  : kHalfF ? kOutLane : NR * (S0 > S1 ? S0 : S1);
+  // the fused gradient's slot-0 contributions (mode 3), staged after the cells
+  constexpr int kContribLane = kGradF && !T::kNoContrib ? 2 * (FusedGrad<K>::S0p / 2) : 0;
+  constexpr int kOutLane1 = kContribLane > kOutLane ? kContribLane : kOutLane;
+  constexpr int kStageLane0 = kCoopLane > kOutLane1 ? kCoopLane : kOutLane1;
   constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
   constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
   __shared__ double stage[kWPB][kWave * kStageLane];
@@ -1080,7 +1105,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (kC0J)  // full aligned chunks returned above
     fast = CSE_C0_VARIANT == 1 && fast && __ballot(act0 || !active) == ~0ull;
   if (!fast) {
-    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
+    StageAndStore<K, kJac, kCrs, kTwoCrs || kHalfF, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;
@@ -1171,8 +1196,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         }
       } else {
         double* st1 = st + kWave * NR * S0;
+        if constexpr (!kHalfF) {
 #pragma unroll
-        for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
+          for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
+        }
         if constexpr (S1 > 0) {
           if constexpr (kLdsE && !kTwo) {
 #pragma unroll
@@ -1184,7 +1211,26 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         }
         seg0 = a.jacobian + (T::kConst0 ? a.fbase[c] : a.jac_base[0][0] + a.jac_stride[0] * i0);
       }
-      if constexpr (!kTwoCrs) {
+      if constexpr (kHalfF) {
+        // Lanes [0, 32) stage their cells, every lane reads the pieces that
+        // fall in them; then lanes [32, 64).
+        constexpr int kHalf = kWave / 2 * NR * S0 / 2;  // pieces per half
+        hp0 = SectorHeadPieces<kA>(seg0);
+        if (lane < kWave / 2) {
+#pragma unroll
+          for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
+        }
+        __builtin_amdgcn_wave_barrier();
+        ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, 0, kHalf, q0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane >= kWave / 2) {
+#pragma unroll
+          for (int p = 0; p < NR * S0; ++p) st[(lane - kWave / 2) * NR * S0 + p] = J0[p];
+        }
+        __builtin_amdgcn_wave_barrier();
+        ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, kHalf, 2 * kHalf, q0);
+      } else if constexpr (!kTwoCrs) {
         __builtin_amdgcn_wave_barrier();
         hp0 = SectorHeadPieces<kA>(seg0);
         ReadSegmentPieces<kQ0, kA>(st, hp0, lane, q0);
@@ -1402,8 +1448,16 @@ __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound
 #ifndef CSE_W1_WAVES_PER_EU
 #define CSE_W1_WAVES_PER_EU 4
 #endif
+// The Snavely camera's Jacobian by hand fits 5 waves per SIMD (88-90 VGPRs,
+// no spills); the held-camera (kConst0) forms and the Jet-based kinds stay at
+// 4 (at 5 the quaternion kinds spill 130-160 bytes a lane).
+#ifndef CSE_FP_W1_WAVES
+#define CSE_FP_W1_WAVES 4
+#endif
+template <class K, class T, int kWaves = CSE_W1_WAVES_PER_EU>
+constexpr int kW1Waves = (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0 && !T::kConst0) ? kWaves : 4;
 template <class K, int kLoss, int kCoop, class T = ShippedTune>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(CSE_W1_WAVES_PER_EU))) void
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T>))) void
 EvaluateAffineChunksTwoRoundW1(const GroupArgs a) {
   static_assert(kTwoRoundBsm<K>, "two-slot kinds");
   AffineChunkBody<K, kLoss, true, false, kCoop, false, T, 1>(a);
@@ -1418,7 +1472,7 @@ __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound
 }
 // The same with one wave per workgroup (6 KiB of LDS each).
 template <class K, int kLoss, int kCoop, class T = ShippedTune>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T>))) void
 EvaluateAffineChunksTwoRoundCrsW1(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, true, kCoop, false, T, 1>(a);
 }
@@ -1452,7 +1506,7 @@ __global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksFusedPoi
 }
 // One wave per workgroup (A/B builds, CSE_FUSEDPOINTS_W1).
 template <class K, int kLoss, bool kCrs, class T = PointsOnlyTune>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T, CSE_FP_W1_WAVES>))) void
 EvaluateAffineChunksFusedPointsW1(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, kCrs, 2, true, T, 1>(a);
 }
@@ -1506,6 +1560,11 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
                                               const double* x1, double* r, double* J0) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1;
+  if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0) {
+    double J1[NR * S1];  // dead: the point's partials are not needed here
+    SnavelyJacobianByHand(d, x0, x1, r, J0, J1);
+    return;
+  }
   Jet<X0> j0[X0], j1[S1], out[NR];
 #pragma unroll
   for (int k = 0; k < X0; ++k) j0[k] = Jet<X0>(x0[k], k);

@@ -183,6 +183,100 @@ struct SnavelyKind {
   CSE_FLAT_FROM_TWO_SLOTS
 };
 
+// SnavelyReprojectionError's residuals and Jacobian blocks written out by
+// hand (the product rule the seeded Jet<12> applies, collected into 3x3
+// matrices): J0 = dr/d[aa, t, f, l1, l2] (2 x 9), J1 = dr/dX (2 x 3), both
+// row-major.  The primal follows Evaluate<double> operation for operation.
+// With p = X + s q + c m + t, q = aa x X, m = aa x q, u = |aa|^2,
+// s(u) = sin(theta)/theta, c(u) = (1 - cos(theta))/theta^2:
+//   dp/dX  = R = (1 - c u) I + s [aa]x + c aa aa^T,
+//   dp/daa = G = w aa^T + c (aa.X) I - [z]x,
+//            w = 2 (s' q + c' m) - c X,  z = s X + c q   (s' = ds/du),
+// exact for every theta: at theta == 0 (s, c, s', c') = (1, 1/2, -1/6, -1/24)
+// give R = I and G = -[X]x, the reference's first-order form.  Then with
+// (xp, yp) = -p_xy / p_z, D = 1 + r2 (l1 + l2 r2):
+//   dr/dp = A B,  A = f (D I + (2 l1 + 4 l2 r2) x x^T),  B = [ni I | ni x],
+// ni = -1/p_z, and J0 = [H G | H | D x | f r2 x | f r2^2 x], J1 = H R.
+CSE_HD bool SnavelyJacobianByHand(const double* obs, const double* cam, const double* X, double* r,
+                                  double* J0, double* J1) {
+  const double a0 = cam[0], a1 = cam[1], a2 = cam[2];
+  const double u = a0 * a0 + a1 * a1 + a2 * a2;
+  double s, c, ds, dc, p[3];
+  // q = aa x X and m = aa x q (the series form's vectors; also G's)
+  const double q0 = a1 * X[2] - a2 * X[1], q1 = a2 * X[0] - a0 * X[2], q2 = a0 * X[1] - a1 * X[0];
+  const double m0 = a1 * q2 - a2 * q1, m1 = a2 * q0 - a0 * q2, m2 = a0 * q1 - a1 * q0;
+  if (u <= 1.0) {
+    RodriguesFactors(u, &s, &c, &ds, &dc);
+    p[0] = X[0] + s * q0 + c * m0;
+    p[1] = X[1] + s * q1 + c * m1;
+    p[2] = X[2] + s * q2 + c * m2;
+  } else {  // AngleAxisRotatePoint's Rodrigues branch for the value
+    const double theta = jhypot(a0, a1, a2);
+    double st, ct;
+    jsincos(theta, &st, &ct);
+    const double ti = 1.0 / theta;
+    const double w0 = a0 * ti, w1 = a1 * ti, w2 = a2 * ti;
+    const double x0 = w1 * X[2] - w2 * X[1], x1 = w2 * X[0] - w0 * X[2], x2 = w0 * X[1] - w1 * X[0];
+    const double tmp = (w0 * X[0] + w1 * X[1] + w2 * X[2]) * (1.0 - ct);
+    p[0] = X[0] * ct + x0 * st + w0 * tmp;
+    p[1] = X[1] * ct + x1 * st + w1 * tmp;
+    p[2] = X[2] * ct + x2 * st + w2 * tmp;
+    s = st * ti;
+    c = (1.0 - ct) / u;
+    ds = (ct - s) / (2.0 * u);
+    dc = (s - 2.0 * c) / (2.0 * u);
+  }
+  p[0] += cam[3];
+  p[1] += cam[4];
+  p[2] += cam[5];
+  // Project<true, double>
+  const double ni = -1.0 / p[2];
+  const double xp = p[0] * ni, yp = p[1] * ni;
+  const double f = cam[6], l1 = cam[7], l2 = cam[8];
+  const double r2 = xp * xp + yp * yp;
+  const double D = 1.0 + r2 * (l1 + l2 * r2);
+  r[0] = f * D * xp - obs[0];
+  r[1] = f * D * yp - obs[1];
+  // H = dr/dp
+  const double fD = f * D, fg = f * (2.0 * l1 + 4.0 * l2 * r2);
+  const double A00 = fD + fg * xp * xp, A01 = fg * xp * yp, A11 = fD + fg * yp * yp;
+  double H[2][3];
+  H[0][0] = A00 * ni;
+  H[0][1] = A01 * ni;
+  H[0][2] = (A00 * xp + A01 * yp) * ni;
+  H[1][0] = A01 * ni;
+  H[1][1] = A11 * ni;
+  H[1][2] = (A01 * xp + A11 * yp) * ni;
+  // R and G
+  const double cu1 = 1.0 - c * u;
+  const double R[3][3] = {{cu1 + c * a0 * a0, c * a0 * a1 - s * a2, c * a0 * a2 + s * a1},
+                          {c * a1 * a0 + s * a2, cu1 + c * a1 * a1, c * a1 * a2 - s * a0},
+                          {c * a2 * a0 - s * a1, c * a2 * a1 + s * a0, cu1 + c * a2 * a2}};
+  const double d = a0 * X[0] + a1 * X[1] + a2 * X[2], cd = c * d;
+  const double w0 = 2.0 * (ds * q0 + dc * m0) - c * X[0];
+  const double w1 = 2.0 * (ds * q1 + dc * m1) - c * X[1];
+  const double w2 = 2.0 * (ds * q2 + dc * m2) - c * X[2];
+  const double z0 = s * X[0] + c * q0, z1 = s * X[1] + c * q1, z2 = s * X[2] + c * q2;
+  const double G[3][3] = {{w0 * a0 + cd, w0 * a1 + z2, w0 * a2 - z1},
+                          {w1 * a0 - z2, w1 * a1 + cd, w1 * a2 + z0},
+                          {w2 * a0 + z1, w2 * a1 - z0, w2 * a2 + cd}};
+  const double xy[2] = {xp, yp};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    double* row = J0 + 9 * k;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      row[j] = H[k][0] * G[0][j] + H[k][1] * G[1][j] + H[k][2] * G[2][j];
+      row[3 + j] = H[k][j];
+      J1[3 * k + j] = H[k][0] * R[0][j] + H[k][1] * R[1][j] + H[k][2] * R[2][j];
+    }
+    row[6] = D * xy[k];
+    row[7] = f * r2 * xy[k];
+    row[8] = f * r2 * r2 * xy[k];
+  }
+  return true;
+}
+
 // SnavelyReprojectionErrorNoRadialDistortion<2, 7, 3>
 // (internal/ceres/evaluator_cuda_test.cu.cc:112-150).
 struct SnavelyNoDistortionKind {

@@ -266,6 +266,12 @@ __device__ __forceinline__ void WaveStore(const double* lds, double* dst, int co
   }
 }
 
+// The Snavely camera's Jacobian on the device: by hand
+// (SnavelyJacobianByHand, CSE_BY_HAND 1) or through the seeded Jets (0).
+#ifndef CSE_BY_HAND
+#define CSE_BY_HAND 1
+#endif
+
 // AutoDifferentiate (include/ceres/internal/autodiff.h:314-381) for the
 // two-slot affine kernels: seed one Jet per parameter with its unit vector,
 // pre-fill the outputs with kImpossibleValue (:355-360), run the functor,
@@ -277,6 +283,10 @@ CSE_HD bool EvaluateFunctor(const double* d, const double* x0, const double* x1,
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1, S1p = Tr::S1p, N = X0 + S1;
   if constexpr (kJac) {
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0)
+      return SnavelyJacobianByHand(d, x0, x1, r, J0, J1);
+#endif
     Jet<N> j0[X0], j1[S1p], out[NR];
 #pragma unroll
     for (int k = 0; k < X0; ++k) j0[k] = Jet<N>(x0[k], k);
