@@ -456,12 +456,6 @@ struct FusedGrad {
 #define CSE_F_HALVES 0
 #endif
 
-// Held-camera tail variants for A/B builds (0: shipped; 1: chunks without
-// a held block take the usual tail from fbase[c], partial sectors and all).
-#ifndef CSE_C0_VARIANT
-#define CSE_C0_VARIANT 0
-#endif
-
 #ifndef CSE_POINT_COPY
 #define CSE_POINT_COPY 0
 #endif
@@ -843,11 +837,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if constexpr (kGradF) fg.Compute(r, J0, J1, in.id1, active, lane, nw, c);
 
   if constexpr (kC0J) {
-    // A/B builds only: CSE_C0_VARIANT 1 sends full chunks without a held
-    // block to the usual tail (seg0 = fbase[c], any 16-byte alignment).
-    bool c0_tail = nw == kWave && C0Aligned(a, fb[2]);
-    if (CSE_C0_VARIANT == 1 && __ballot(act0 || !active) == ~0ull) c0_tail = false;
-    if (c0_tail) {
+    if (nw == kWave && C0Aligned(a, fb[2])) {
       // ---- held-camera groups, full chunk: whole-sector windows ----
       // After a held block the packed F cells (BSM) or row blocks (CRS) no
       // longer start on 64-byte sectors.  The wave stores only the whole
@@ -1102,8 +1092,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     }
   }
   bool fast = FastTail<K, kJac, kCrs, T::kConst0>(a, i0, nw, c);
-  if constexpr (kC0J)  // full aligned chunks returned above
-    fast = CSE_C0_VARIANT == 1 && fast && __ballot(act0 || !active) == ~0ull;
+  if constexpr (kC0J) fast = false;  // full aligned chunks returned above
   if (!fast) {
     StageAndStore<K, kJac, kCrs, kTwoCrs || kHalfF, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
     if constexpr (kGradF) {

@@ -323,6 +323,22 @@ CSE_HD bool EvaluateFunctorFlat(const double* d, const double* x, double* r, dou
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, N = Tr::N;
   if constexpr (kJac) {
+#ifdef __HIP_DEVICE_COMPILE__
+    // The same arithmetic as the affine kernels (EvaluateFunctor): the two
+    // store paths write bit-identical Jacobians.
+    if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0) {
+      double J0[18], J1[6];
+      const bool ok = SnavelyJacobianByHand(d, x, x + 9, r, J0, J1);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+#pragma unroll
+        for (int c = 0; c < 9; ++c) J[k * N + c] = J0[9 * k + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) J[k * N + 9 + c] = J1[3 * k + c];
+      }
+      return ok;
+    }
+#endif
     Jet<N> xj[N], out[NR];
 #pragma unroll
     for (int k = 0; k < N; ++k) xj[k] = Jet<N>(x[k], k);
