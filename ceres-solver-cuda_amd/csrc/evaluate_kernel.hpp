@@ -142,23 +142,12 @@ __device__ __forceinline__ void StageAndStore(const GroupArgs& a, double* st, in
         __builtin_amdgcn_wave_barrier();
         WaveStore(st, a.jacobian + a.fbase[c], __popcll(m) * NR * S0, lane);
       } else {
-        constexpr int kParts = kHalves ? 2 : 1, kLanes = kWave / kParts;
+        if (active) {
 #pragma unroll
-        for (int h = 0; h < kParts; ++h) {
-          const int lo = h * kLanes;
-          const int cnt = nw - lo < kLanes ? nw - lo : kLanes;
-          if (cnt <= 0) break;
-          if (h > 0) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-          }
-          if (active && lane >= lo && lane < lo + kLanes) {
-#pragma unroll
-            for (int q = 0; q < NR * S0; ++q) st[(lane - lo) * NR * S0 + q] = J0[q];
-          }
-          __builtin_amdgcn_wave_barrier();
-          WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * (i0 + lo), cnt * NR * S0, lane);
+          for (int q = 0; q < NR * S0; ++q) st[lane * NR * S0 + q] = J0[q];
         }
+        __builtin_amdgcn_wave_barrier();
+        WaveStore(st, a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * i0, nw * NR * S0, lane);
       }
       if constexpr (S1 > 0) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -450,10 +439,25 @@ struct FusedGrad {
 // per gradient evaluation, profiles/round4/r4g/ab_grad) -- the camera
 // kernel's 24-byte point gathers already cost one sector request each, so a
 // sector-aligned copy saves no requests; -DCSE_POINT_COPY=1 builds it.
-// BlockSparseMatrix F cells staged for lanes [0, 32), then [32, 64), through
-// half the LDS (1), or for the whole wave at once (0).
-#ifndef CSE_F_HALVES
-#define CSE_F_HALVES 0
+// Waves per CU of the one-wave Jacobian kernels, capped through their LDS
+// footprint (doubles a lane; 0 = no cap).  BSM: 26 (13 KiB, 12 waves per
+// CU): with the by-hand Snavely functor the kernel needs only 92 VGPRs, and
+// more resident waves write the BSM's three output streams (F cells, E
+// cells, residuals) slower -- 1.400 ms at 12 waves per CU, 1.405-1.418 at
+// 11, 1.44 at 13-14, 1.50 at 16, 1.525 at 17 (LDS-bound), 1.555 at 20, and
+// 1.427 for the Jet kernel at 16 (profiles/round4/r4occ, r4occ2, r4s7).
+// CRS (one output stream) is fastest uncapped (20 waves per CU).
+#ifndef CSE_STAGE_MIN_LANE
+#define CSE_STAGE_MIN_LANE 26
+#endif
+#ifndef CSE_STAGE_MIN_LANE_CRS
+#define CSE_STAGE_MIN_LANE_CRS 0
+#endif
+#ifndef CSE_STAGE_MIN_LANE_FP
+#define CSE_STAGE_MIN_LANE_FP 0
+#endif
+#ifndef CSE_STAGE_MIN_LANE_C0
+#define CSE_STAGE_MIN_LANE_C0 0
 #endif
 
 #ifndef CSE_POINT_COPY
@@ -691,25 +695,27 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   // CRS rows staged in two halves of the wave (lanes [0, 32), then [32, 64)).
   constexpr bool kTwoCrs = T::kTwoRound && kJac && kCrs;
   constexpr int kA = T::kAlign;
-  // BSM F cells in two half-wave rounds (CSE_F_HALVES; not the held-camera
-  // kernels, which stage compacted cells).
-  constexpr bool kHalfF = CSE_F_HALVES != 0 && kTwo && !T::kConst0 && (NR * S0) % 2 == 0;
   constexpr int kOutLane = kJac ? (kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N)
-                                        : kHalfF ? (NR * S0 / 2 > NR * S1 ? NR * S0 / 2 : NR * S1)
                                         : kTwo ? NR * (S0 > S1 ? S0 : S1)
                                                : kLdsE ? NR * (S0 + S1) : NR * S0)
                                 : 1;
   constexpr int kCoopLane = kCoop == 2 ? ((Tr::X0 + 1) & ~1) : Tr::X0;
   // StageAndStore's footprint (ragged chunks): whole rows (CRS) or one
   // slot's cells at a time (BSM).
-  constexpr int kSlowLane = !kJac ? 1 : kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N)
-                                  : kHalfF ? kOutLane : NR * (S0 > S1 ? S0 : S1);
+  constexpr int kSlowLane = !kJac ? 1 : kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N) : NR * (S0 > S1 ? S0 : S1);
   // the fused gradient's slot-0 contributions (mode 3), staged after the cells
   constexpr int kContribLane = kGradF && !T::kNoContrib ? 2 * (FusedGrad<K>::S0p / 2) : 0;
   constexpr int kOutLane1 = kContribLane > kOutLane ? kContribLane : kOutLane;
   constexpr int kStageLane0 = kCoopLane > kOutLane1 ? kCoopLane : kOutLane1;
   constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
-  constexpr int kStageLane = T::kMinLane > kStageLane1 ? T::kMinLane : kStageLane1;
+  // The LDS cap on waves per CU (CSE_STAGE_MIN_LANE, above); the fused
+  // gradient's points kernel measured neutral to it (r4s7).
+  constexpr int kPadLane = kWPB != 1 || !kJac ? 0
+                          : T::kConst0 ? (kGradF || kCrs ? 0 : CSE_STAGE_MIN_LANE_C0)
+                          : kGradF ? CSE_STAGE_MIN_LANE_FP
+                          : kCrs ? CSE_STAGE_MIN_LANE_CRS : CSE_STAGE_MIN_LANE;
+  constexpr int kMinLane = kPadLane > T::kMinLane ? kPadLane : T::kMinLane;
+  constexpr int kStageLane = kMinLane > kStageLane1 ? kMinLane : kStageLane1;
   __shared__ double stage[kWPB][kWave * kStageLane];
 
   constexpr bool kC0J = T::kConst0 && kJac;
@@ -1094,7 +1100,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   bool fast = FastTail<K, kJac, kCrs, T::kConst0>(a, i0, nw, c);
   if constexpr (kC0J) fast = false;  // full aligned chunks returned above
   if (!fast) {
-    StageAndStore<K, kJac, kCrs, kTwoCrs || kHalfF, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
+    StageAndStore<K, kJac, kCrs, kTwoCrs, T::kConst0>(a, st, lane, active, i0, nw, r, J0, J1, act0, c);
     if constexpr (kGradF) {
       // The group's last, partial chunk: plain stores.
       constexpr int S0p = FusedGrad<K>::S0p;
@@ -1185,10 +1191,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         }
       } else {
         double* st1 = st + kWave * NR * S0;
-        if constexpr (!kHalfF) {
 #pragma unroll
-          for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
-        }
+        for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
         if constexpr (S1 > 0) {
           if constexpr (kLdsE && !kTwo) {
 #pragma unroll
@@ -1200,26 +1204,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         }
         seg0 = a.jacobian + (T::kConst0 ? a.fbase[c] : a.jac_base[0][0] + a.jac_stride[0] * i0);
       }
-      if constexpr (kHalfF) {
-        // Lanes [0, 32) stage their cells, every lane reads the pieces that
-        // fall in them; then lanes [32, 64).
-        constexpr int kHalf = kWave / 2 * NR * S0 / 2;  // pieces per half
-        hp0 = SectorHeadPieces<kA>(seg0);
-        if (lane < kWave / 2) {
-#pragma unroll
-          for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
-        }
-        __builtin_amdgcn_wave_barrier();
-        ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, 0, kHalf, q0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (lane >= kWave / 2) {
-#pragma unroll
-          for (int p = 0; p < NR * S0; ++p) st[(lane - kWave / 2) * NR * S0 + p] = J0[p];
-        }
-        __builtin_amdgcn_wave_barrier();
-        ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, kHalf, 2 * kHalf, q0);
-      } else if constexpr (!kTwoCrs) {
+      if constexpr (!kTwoCrs) {
         __builtin_amdgcn_wave_barrier();
         hp0 = SectorHeadPieces<kA>(seg0);
         ReadSegmentPieces<kQ0, kA>(st, hp0, lane, q0);
