@@ -456,8 +456,10 @@ struct FusedGrad {
 #ifndef CSE_STAGE_MIN_LANE_FP
 #define CSE_STAGE_MIN_LANE_FP 0
 #endif
+// The held-camera BSM kernel likewise: 1.444-1.447 ms capped at 12 against
+// 1.51-1.54 uncapped (16 per CU; profiles/round4/r4s8).
 #ifndef CSE_STAGE_MIN_LANE_C0
-#define CSE_STAGE_MIN_LANE_C0 0
+#define CSE_STAGE_MIN_LANE_C0 26
 #endif
 
 #ifndef CSE_POINT_COPY
