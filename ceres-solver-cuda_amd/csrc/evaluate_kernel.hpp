@@ -710,9 +710,12 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   constexpr int kOutLane1 = kContribLane > kOutLane ? kContribLane : kOutLane;
   constexpr int kStageLane0 = kCoopLane > kOutLane1 ? kCoopLane : kOutLane1;
   constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
-  // The LDS cap on waves per CU (CSE_STAGE_MIN_LANE, above); the fused
-  // gradient's points kernel measured neutral to it (r4s7).
-  constexpr int kPadLane = kWPB != 1 || !kJac ? 0
+  // The LDS cap on waves per CU (CSE_STAGE_MIN_LANE, above), for the
+  // by-hand Snavely kernels only (the Jet-based quaternion kernel is
+  // register-bound at 16 waves per CU and slower capped: 1.516 vs 1.38 ms,
+  // r4s9); the fused gradient's points kernel measured neutral to it (r4s7).
+  constexpr bool kByHand = std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0;
+  constexpr int kPadLane = kWPB != 1 || !kJac || !kByHand ? 0
                           : T::kConst0 ? (kGradF || kCrs ? 0 : CSE_STAGE_MIN_LANE_C0)
                           : kGradF ? CSE_STAGE_MIN_LANE_FP
                           : kCrs ? CSE_STAGE_MIN_LANE_CRS : CSE_STAGE_MIN_LANE;
