@@ -458,6 +458,12 @@ struct FusedGrad {
 #endif
 // The held-camera BSM kernel likewise: 1.444-1.447 ms capped at 12 against
 // 1.51-1.54 uncapped (16 per CU; profiles/round4/r4s8).
+// The residual-only and cost-only kernels (8 waves per SIMD, 60 VGPRs) are
+// fastest uncapped: capped at 24 waves per CU alike, at 16 7-15 % slower
+// (profiles/round4/r4res).
+#ifndef CSE_STAGE_MIN_LANE_RES
+#define CSE_STAGE_MIN_LANE_RES 0
+#endif
 #ifndef CSE_STAGE_MIN_LANE_C0
 #define CSE_STAGE_MIN_LANE_C0 26
 #endif
@@ -715,7 +721,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   // register-bound at 16 waves per CU and slower capped: 1.516 vs 1.38 ms,
   // r4s9); the fused gradient's points kernel measured neutral to it (r4s7).
   constexpr bool kByHand = std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0;
-  constexpr int kPadLane = kWPB != 1 || !kJac || !kByHand ? 0
+  constexpr int kPadLane = !kJac ? (std::is_same<K, SnavelyKind>::value ? CSE_STAGE_MIN_LANE_RES : 0)
+                          : kWPB != 1 || !kByHand ? 0
                           : T::kConst0 ? (kGradF || kCrs ? 0 : CSE_STAGE_MIN_LANE_C0)
                           : kGradF ? CSE_STAGE_MIN_LANE_FP
                           : kCrs ? CSE_STAGE_MIN_LANE_CRS : CSE_STAGE_MIN_LANE;
@@ -1562,8 +1569,14 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
   }
 }
 
+// CSE_CAMGRAD_WAVES: a lower bound on its waves per SIMD (A/B builds; 1 = the
+// compiler's choice, 158 VGPRs = 3 with the by-hand functor).
+#ifndef CSE_CAMGRAD_WAVES
+#define CSE_CAMGRAD_WAVES 1
+#endif
 template <class K, int kLoss, int kWPB = kWavesPerBlock>
-__global__ __launch_bounds__(kWPB * kWave) void CameraGradientKernel(const CamGradArgs g) {
+__global__ __launch_bounds__(kWPB * kWave) __attribute__((amdgpu_waves_per_eu(CSE_CAMGRAD_WAVES))) void
+CameraGradientKernel(const CamGradArgs g) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, D = Tr::D;
   static_assert(Tr::NB == 2 && S1 > 0, "two-slot kinds");
