@@ -450,6 +450,10 @@ struct FusedGrad {
 #ifndef CSE_STAGE_MIN_LANE
 #define CSE_STAGE_MIN_LANE 26
 #endif
+// A/B builds: the Jacobian kernels' chunks in XCD-contiguous ranges (1).
+#ifndef CSE_XCD_MAP
+#define CSE_XCD_MAP 0
+#endif
 #ifndef CSE_STAGE_MIN_LANE_CRS
 #define CSE_STAGE_MIN_LANE_CRS 0
 #endif
@@ -734,7 +738,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
-  const int64_t wg = T::kXcdMap ? XcdContiguous(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t wg = (T::kXcdMap || (CSE_XCD_MAP != 0 && kJac)) ? XcdContiguous(blockIdx.x, gridDim.x)
+                                                                 : (int64_t)blockIdx.x;
   const int64_t c = wg * kWPB + wave;
   double* partial_dst = a.partials + c;
   if (c >= num_chunks) {
