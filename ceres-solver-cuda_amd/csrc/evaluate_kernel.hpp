@@ -440,15 +440,18 @@ struct FusedGrad {
 // kernel's 24-byte point gathers already cost one sector request each, so a
 // sector-aligned copy saves no requests; -DCSE_POINT_COPY=1 builds it.
 // Waves per CU of the one-wave Jacobian kernels, capped through their LDS
-// footprint (doubles a lane; 0 = no cap).  BSM: 26 (13 KiB, 12 waves per
-// CU): with the by-hand Snavely functor the kernel needs only 92 VGPRs, and
-// more resident waves write the BSM's three output streams (F cells, E
-// cells, residuals) slower -- 1.400 ms at 12 waves per CU, 1.405-1.418 at
-// 11, 1.44 at 13-14, 1.50 at 16, 1.525 at 17 (LDS-bound), 1.555 at 20, and
-// 1.427 for the Jet kernel at 16 (profiles/round4/r4occ, r4occ2, r4s7).
-// CRS (one output stream) is fastest uncapped (20 waves per CU).
+// footprint (doubles a lane; 0 = no cap).  BSM: 20 (10 KiB, 16 waves per
+// CU).  With the by-hand Snavely functor the kernel needs only 92 VGPRs and
+// could keep 17 waves per CU resident (LDS-bound); how many should depends on
+// how the resident waves' three output streams (F cells, E cells, residuals)
+// interleave.  With the tail storing F, E, residuals: 1.400 ms at 12 waves
+// per CU, 1.44 at 13-14, 1.50 at 16, 1.525 at 17 (profiles/round4/r4occ,
+// r4occ2, r4s7; the Jet kernel 1.427 at 16).  Storing E first (E, F,
+// residuals; CSE_STORE_ORDER 2): 1.346-1.354 at 12, 1.326-1.336 at 14,
+// 1.314-1.321 at 16 (r4ord2), and 16 ahead of 15 and 17 on another box
+// (r4ord3).  CRS (one output stream) is fastest uncapped (20 waves per CU).
 #ifndef CSE_STAGE_MIN_LANE
-#define CSE_STAGE_MIN_LANE 26
+#define CSE_STAGE_MIN_LANE 20
 #endif
 // A/B builds: the Jacobian kernels' chunks in XCD-contiguous ranges (1).
 #ifndef CSE_XCD_MAP
@@ -459,6 +462,10 @@ struct FusedGrad {
 #endif
 #ifndef CSE_STAGE_MIN_LANE_FP
 #define CSE_STAGE_MIN_LANE_FP 0
+#endif
+// The held-camera tail's E cells before its F window (1) or after (0).
+#ifndef CSE_C0_E_FIRST
+#define CSE_C0_E_FIRST 0
 #endif
 // The held-camera BSM kernel likewise: 1.444-1.447 ms capped at 12 against
 // 1.51-1.54 uncapped (16 per CU; profiles/round4/r4s8).
@@ -659,7 +666,14 @@ __device__ __forceinline__ int64_t XcdContiguous(int64_t b, int64_t nwg) {
 // wave), which with the kernel held to 128 VGPRs (EvaluateAffineChunksTwoRound)
 // gives 4 waves per SIMD instead of 3.  That was neutral with the heavier
 // functor (s3i, s3j) and is 2.5 % faster with the series rotation (s4n).
-using ShippedTune = Tune<0, true, true>;
+// The store tail's segment order: 0 = F, E, residuals; 1 = residuals, E, F;
+// 2 = E, F, residuals (shipped: with the BSM kernel at 12 waves per CU,
+// 1.369-1.373 ms against 1.397-1.398 for 0 and 1.369-1.377 for 1; CRS
+// neutral; profiles/round4/r4ord).
+#ifndef CSE_STORE_ORDER
+#define CSE_STORE_ORDER 2
+#endif
+using ShippedTune = Tune<0, true, true, 0, 64, CSE_STORE_ORDER>;
 // The fused gradient's points-only form (CameraGradientKernel adds slot 0).
 using PointsOnlyTune = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true>;
 // The same for groups with constant slot-0 blocks (a held camera): a wave
@@ -1083,11 +1097,12 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       // neutral, profiles/round4/r4s5.)
       if (jacw && lane < 8) StoreNt16<0, 1>(ws, qs);
       if (jacw) {
+        if constexpr (!kCrs && CSE_C0_E_FIRST != 0) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
         if (whole)
           SegmentStoresMasked<0, kQF>(wf0, wf1, qf, 0, kQF * kWave);  // no lane masked
         else
           SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
-        if constexpr (!kCrs) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
+        if constexpr (!kCrs && CSE_C0_E_FIRST == 0) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
       }
       if (a.residuals) StoreNt16<0>(rdst, qr);  // a full chunk: every lane active
       store_g();
