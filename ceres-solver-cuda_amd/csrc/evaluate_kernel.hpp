@@ -463,9 +463,11 @@ struct FusedGrad {
 #ifndef CSE_STAGE_MIN_LANE_FP
 #define CSE_STAGE_MIN_LANE_FP 0
 #endif
-// The held-camera tail's E cells before its F window (1) or after (0).
+// The held-camera tail's E cells before its F window (1, shipped: held
+// evaluation 1.435-1.439 against 1.462-1.471 ms with E after F, the unheld
+// evaluation 1.425-1.427 on that box; profiles/round4/r4held5) or after (0).
 #ifndef CSE_C0_E_FIRST
-#define CSE_C0_E_FIRST 0
+#define CSE_C0_E_FIRST 1
 #endif
 // The held-camera BSM kernel likewise: 1.444-1.447 ms capped at 12 against
 // 1.51-1.54 uncapped (16 per CU; profiles/round4/r4s8).
