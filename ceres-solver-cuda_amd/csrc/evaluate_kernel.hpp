@@ -460,8 +460,13 @@ struct FusedGrad {
 #ifndef CSE_STAGE_MIN_LANE_CRS
 #define CSE_STAGE_MIN_LANE_CRS 0
 #endif
+// The fused gradient's points kernel (94 VGPRs by hand): capped at 16 waves
+// per CU like the Jet kernel's register bound (uncapped, 17, the gradient
+// evaluation took 2.157-2.163 ms against 2.119-2.124 for the Jet build,
+// profiles/round4/r4grad2; capped at 16, 2.126-2.133 against 2.124-2.131,
+// r4s7).
 #ifndef CSE_STAGE_MIN_LANE_FP
-#define CSE_STAGE_MIN_LANE_FP 0
+#define CSE_STAGE_MIN_LANE_FP 20
 #endif
 // The held-camera tail's E cells before its F window (1, shipped: held
 // evaluation 1.435-1.439 against 1.462-1.471 ms with E after F, the unheld
@@ -1519,6 +1524,12 @@ EvaluateAffineChunksFusedPointsW1(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, kCrs, 2, true, T, 1>(a);
 }
 
+// The camera-order re-evaluation's Jacobian: by hand (1) or through Jet<9>
+// with the point constant (0).
+#ifndef CSE_BY_HAND_CAMGRAD
+#define CSE_BY_HAND_CAMGRAD 1
+#endif
+
 // Slot-0 (camera) part of the fused gradient, by re-evaluation in camera
 // order.  The evaluation kernel runs in block (point) order, in which a
 // camera's ~2,100 blocks are spread over the whole problem; summing their
@@ -1568,7 +1579,7 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
                                               const double* x1, double* r, double* J0) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1;
-  if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0) {
+  if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0 && CSE_BY_HAND_CAMGRAD != 0) {
     double J1[NR * S1];  // dead: the point's partials are not needed here
     SnavelyJacobianByHand(d, x0, x1, r, J0, J1);
     return;
