@@ -682,7 +682,13 @@ __device__ __forceinline__ int64_t XcdContiguous(int64_t b, int64_t nwg) {
 #endif
 using ShippedTune = Tune<0, true, true, 0, 64, CSE_STORE_ORDER>;
 // The fused gradient's points-only form (CameraGradientKernel adds slot 0).
-using PointsOnlyTune = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true>;
+// Its store order (as CSE_STORE_ORDER): residuals, E, F (1) -- gradient
+// evaluation 1.965-1.970 ms against 2.017-2.026 for F, E, residuals (0) and
+// 1.976-1.978 for E, F, residuals (2), same box (profiles/round4/r4fpord).
+#ifndef CSE_FP_STORE_ORDER
+#define CSE_FP_STORE_ORDER 1
+#endif
+using PointsOnlyTune = Tune<0, true, true, 0, 64, CSE_FP_STORE_ORDER, false, false, 0, 0, false, true>;
 // The same for groups with constant slot-0 blocks (a held camera): a wave
 // with one takes the slow tail, its F cells packed from fbase[c]; waves
 // without take the fast tail from fbase[c].
