@@ -24,10 +24,10 @@
 
 #include "../../include/cse.h"
 #include "multi_device.h"
-#include "persistent_launch.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
-#include "../../tools/tuning/pipeline_launch.h"  // tuning build only
+#include "../../tools/tuning/persistent_launch.h"  // tuning build only
+#include "../../tools/tuning/pipeline_launch.h"    // tuning build only
 #endif
 
 namespace {
@@ -322,6 +322,17 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
   (void)num_wg;
   cse::LaunchPipelinedSnavelyProbe<L, kStoreWaves, kOpt>(a, s);
 }
+
+// Tuning build: the BlockSparseMatrix Jacobian evaluation of the Snavely
+// camera as persistent software-pipelined waves, two chunks in flight per
+// wave (tools/tuning/persistent_kernel.hpp, its own TU; measured 18 %
+// slower than the shipped kernel).  Variant 70.
+template <class K, int L>
+void LaunchPersistent(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  static_assert(std::is_same<K, cse::SnavelyKind>::value, "Snavely only");
+  (void)num_wg;
+  cse::LaunchPersistentSnavely<L>(a, s);
+}
 #endif
 
 // The shipped CRS Jacobian kernel (two half-wave staging rounds, 4 waves
@@ -363,28 +374,6 @@ void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   } else {
     hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPoints<K, L, Crs, T>), dim3((unsigned)num_wg),
                        dim3(cse::kBlockThreads), 0, s, a);
-  }
-}
-
-// The BlockSparseMatrix Jacobian evaluation of the Snavely camera
-// (residuals and Jacobian, no gradient, no held cameras) as persistent
-// software-pipelined waves (persistent_kernel.hpp, its own TU
-// persistent.hip): CSE_PERSISTENT 1; 0 keeps the one-chunk-per-wave kernel.
-#ifndef CSE_PERSISTENT
-#define CSE_PERSISTENT 0
-#endif
-template <int L>
-void LaunchPersistent(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  (void)num_wg;
-  cse::LaunchPersistentSnavely<L>(a, s);
-}
-
-LaunchFn PickPersistent(int kind, int loss) {
-  if (kind != CSE_FUNCTOR_SNAVELY_2_9_3) return nullptr;
-  switch (loss) {
-    case CSE_LOSS_HUBER: return &LaunchPersistent<cse::kLossHuber>;
-    case CSE_LOSS_CAUCHY: return &LaunchPersistent<cse::kLossCauchy>;
-    default: return &LaunchPersistent<cse::kLossTrivial>;
   }
 }
 
@@ -548,6 +537,16 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 48: return &LaunchPipelined<K, L, 4, 2>;
     case 49: return &LaunchPipelined<K, L, 6, 2>;
     case 50: return &LaunchPipelinedProbe<K, L, 8, 2>;
+    // persistent same-wave double buffering (tools/tuning/persistent.hip)
+    case 70: return &LaunchPersistent<K, L>;
+    // The removal breakdown on the shipped kernel (EvaluateAffineChunksTwoRoundW1,
+    // ShippedTune's settings): kDiag 1 functor replaced by a few additions,
+    // 2 no camera gather, 3 both, 4 no Jacobian stores, 5 no E-cell stores.
+    case 81: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 1>>;
+    case 82: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 2>>;
+    case 83: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 3>>;
+    case 84: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 4>>;
+    case 85: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 5>>;
     default: return nullptr;
   }
 }
@@ -1407,9 +1406,6 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     if (G.const0 && !fused) grad_pass = false;
     const bool recompute = fused && mode != 3;  // slot 0 by CameraGradientKernel
     cse::GroupArgs a = MakeArgs(ev, G, d_state, d_res, d_jac, grad_pass ? nullptr : d_grad);
-    if (CSE_PERSISTENT != 0 && d_jac && d_res && !d_grad && G.policy == kAffinePacked && dma &&
-        !G.const0)
-      if (LaunchFn pf = PickPersistent(G.kind, G.loss.kind)) fn = pf;
     if (fused) {
       const int64_t chunks = (G.n + cse::kWave - 1) / cse::kWave;
       int rc;

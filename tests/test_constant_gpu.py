@@ -239,9 +239,20 @@ def test_problem_13682_one_held_camera(gpu):
     """problem-13682 with its first camera held (the gauge), Huber, BSM."""
     prog = bal.synthetic_program("problem-13682-4456117", loss=ca.Loss.huber(1.0),
                                  constant_cameras=(0,))
-    got, info = gpu_eval(prog)
+    ev = ca.Evaluator(prog)
+    try:
+        got = ev.evaluate()
+        info = ev.info()
+        # The residual+Jacobian kernel without the gradient (the held-camera
+        # form of EvaluateAffineChunksTwoRoundW1 and HeldSectorFixupKernel).
+        ok, cost, r, _, j = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    finally:
+        ev.close()
     assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
     ref = oracle_eval(prog, threads=16)
-    rep = {}
+    rep, rep_ng = {}, {}
     assert_parity(got, ref, "problem-13682 held camera", report=rep)
+    assert_parity((ok, cost, r, None, j), (ref[0], ref[1], ref[2], None, ref[4]),
+                  "problem-13682 held camera, no gradient", report=rep_ng)
     print("problem-13682 one-held-camera parity:", rep)
+    print("problem-13682 one-held-camera parity, residual+Jacobian kernel:", rep_ng)

@@ -225,6 +225,9 @@ def test_configs4_problem_13682_cse_create_multi_8_shards(gpu, problem_13682):
     first, devs = ev.shard_info()
     got = ev.evaluate(residuals=True, gradient=True, jacobian=True)
     info = ev.info()
+    # Each shard's residual+Jacobian kernel without the gradient (the
+    # kernel bench.py times), assembled into the caller's buffers.
+    ok_ng, cost_ng, r_ng, _, j_ng = ev.evaluate(residuals=True, gradient=False, jacobian=True)
     ev.close()
     assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
     assert len(first) == 9 and (np.diff(first) > 0).all()
@@ -235,6 +238,10 @@ def test_configs4_problem_13682_cse_create_multi_8_shards(gpu, problem_13682):
     rep = {}
     assert_parity(got, ref, "configs[4] cse_create_multi x8", report=rep)
     print("configs[4] (cse_create_multi, 8 shards) BSM Huber parity:", rep, "cuts", list(first))
+    rep_ng = {}
+    assert_parity((ok_ng, cost_ng, r_ng, None, j_ng), (ref[0], ref[1], ref[2], None, ref[4]),
+                  "configs[4] cse_create_multi x8, no gradient", report=rep_ng)
+    print("configs[4] (cse_create_multi, 8 shards), residual+Jacobian kernel:", rep_ng)
 
 
 @pytest.mark.slow
@@ -246,32 +253,44 @@ def test_configs4_problem_13682_per_rank_shards(gpu, problem_13682, fmt):
     cams, pts, ci, pi, obs = problem_13682
     world = 8
     loss = ca.Loss.huber(1.0)
-    parts = []
-    cost = 0.0
+    parts, parts_ng = [], []
+    cost = cost_ng = 0.0
     cam_rows = None
     for rank in range(world):
         prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss, format=fmt)
         ev = ca.Evaluator(prog, device=0)
         ok, c, r, g, j = ev.evaluate(residuals=True, gradient=True, jacobian=True)
         info = ev.info()
+        # The rank's timed evaluation (bench.py --gpus 8): residuals and
+        # Jacobian, no gradient (EvaluateAffineChunksTwoRoundW1 / ...CrsW1).
+        ok_ng, c_ng, r_ng, _, j_ng = ev.evaluate(residuals=True, gradient=False, jacobian=True)
         ev.close()
-        assert ok and info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
+        assert ok and ok_ng and info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
         cost += c  # the all-reduce, in rank order
+        cost_ng += c_ng
         npts = sh.points[1] - sh.points[0]
         rows = g[3 * npts:]
         cam_rows = rows.copy() if cam_rows is None else cam_rows + rows
         parts.append((sh, r, j, g[:3 * npts].copy()))
+        parts_ng.append((r_ng, j_ng))
         del prog
     assert len({p[0].blocks for p in parts}) == world
     assert all(p[0].blocks[0] % 4 == 0 for p in parts)
     full = bal.program(cams, pts, ci, pi, obs, loss=loss, format=fmt)
-    J = shard.assemble([p[0] for p in parts], [p[2] for p in parts], full.num_jacobian_values)
-    assert not np.isnan(J).any()
-    R = np.full(full.num_residuals, np.nan)
-    for sh, r, _, _ in parts:
-        r0, r1 = sh.residual_strip
-        R[r0:r1] = r
-    assert not np.isnan(R).any()
+
+    def assemble(res, jac):
+        J = shard.assemble([p[0] for p in parts], jac, full.num_jacobian_values)
+        assert not np.isnan(J).any()
+        R = np.full(full.num_residuals, np.nan)
+        for p, r in zip(parts, res):
+            r0, r1 = p[0].residual_strip
+            R[r0:r1] = r
+        assert not np.isnan(R).any()
+        return R, J
+
+    R, J = assemble([p[1] for p in parts], [p[2] for p in parts])
+    R_ng, J_ng = assemble([p[0] for p in parts_ng], [p[1] for p in parts_ng])
+    del parts_ng
     from ceres_amd import distributed
     G = distributed.assemble_gradient([p[0] for p in parts], [p[3] for p in parts], cam_rows,
                                       pts.shape[0], cams.shape[0])
@@ -280,3 +299,7 @@ def test_configs4_problem_13682_per_rank_shards(gpu, problem_13682, fmt):
     rep = {}
     assert_parity((True, cost, R, G, J), ref, ("configs[4] per-rank shards", fmt), report=rep)
     print(f"configs[4] (8 per-rank shards) {fmt} Huber parity:", rep)
+    rep_ng = {}
+    assert_parity((True, cost_ng, R_ng, None, J_ng), (ref[0], ref[1], ref[2], None, ref[4]),
+                  ("configs[4] per-rank shards, no gradient", fmt), report=rep_ng)
+    print(f"configs[4] (8 per-rank shards) {fmt} Huber, residual+Jacobian kernel:", rep_ng)

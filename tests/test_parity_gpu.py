@@ -32,6 +32,13 @@ def oracle_eval(prog, threads=8, apply_loss=True, **kw):
                        num_threads=threads, **kw)
 
 
+def drop_gradient(out):
+    """(ok, cost, r, g, j) without the gradient, for evaluations that did not
+    request it."""
+    ok, cost, r, _, j = out
+    return ok, cost, r, None, j
+
+
 def gpu_eval(prog, **kw):
     opts = {k: kw.pop(k) for k in list(kw) if k in ("force_general_layout", "apply_loss_function",
                                                     "check_finite")}
@@ -80,10 +87,22 @@ def test_problem_1778_compressed_row_huber(gpu):
     prog = bal.synthetic_program("problem-1778-993923", loss=ca.Loss.huber(1.0),
                                  format=ca.COMPRESSED_ROW)
     ref = oracle_eval(prog, threads=16)
-    got, _ = gpu_eval(prog)
-    rep = {}
+    ev = ca.Evaluator(prog)
+    try:
+        got = ev.evaluate()
+        # The timed evaluation of bench.py's secondary.configs2 (residuals and
+        # Jacobian, no gradient: EvaluateAffineChunksTwoRoundCrsW1), the
+        # Jacobian evaluation at an accepted point (trust_region_minimizer.cc:
+        # 822-826).
+        got_ng = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    finally:
+        ev.close()
+    rep, rep_ng = {}, {}
     assert_parity(got, ref, "problem-1778", report=rep)
+    assert_parity(drop_gradient(got_ng), drop_gradient(ref), "problem-1778 no gradient",
+                  report=rep_ng)
     print("problem-1778 CRS Huber parity:", rep)
+    print("problem-1778 CRS Huber parity, residual+Jacobian kernel:", rep_ng)
 
 
 @pytest.mark.parametrize("combo", range(8))
@@ -337,13 +356,26 @@ def test_problem_13682_full_size(gpu):
     O_ = prog.num_residual_blocks
     assert prog.num_jacobian_values == 24 * O_
     # The gradient comes from the fused deterministic path (gradient_mode 0),
-    # as in a trust-region Jacobian evaluation.
-    got, info = gpu_eval(prog, residuals=True, gradient=True, jacobian=True)
+    # as in a trust-region Jacobian evaluation; then the headline evaluation
+    # bench.py times (residuals and Jacobian, no gradient:
+    # EvaluateAffineChunksTwoRoundW1 over all 28,987,644 blocks), as
+    # TrustRegionMinimizer issues it at an accepted point
+    # (trust_region_minimizer.cc:822-826).
+    ev = ca.Evaluator(prog)
+    try:
+        got = ev.evaluate(residuals=True, gradient=True, jacobian=True)
+        info = ev.info()
+        got_ng = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    finally:
+        ev.close()
     assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
     ref = oracle_eval(prog, threads=16, residuals=True, gradient=True, jacobian=True)
-    rep = {}
+    rep, rep_ng = {}, {}
     assert_parity(got, ref, "problem-13682", report=rep)
+    assert_parity(drop_gradient(got_ng), drop_gradient(ref), "problem-13682 no gradient",
+                  report=rep_ng)
     print("problem-13682 BSM Huber parity:", rep)
+    print("problem-13682 BSM Huber parity, residual+Jacobian kernel:", rep_ng)
 
 
 def test_gradient_post_pass_deterministic_and_agrees_with_atomics(gpu):

@@ -22,7 +22,7 @@
 #ifndef CSE_PERSISTENT_KERNEL_HPP_
 #define CSE_PERSISTENT_KERNEL_HPP_
 
-#include "evaluate_kernel.hpp"
+#include "../../ceres-solver-cuda_amd/csrc/evaluate_kernel.hpp"
 
 namespace cse {
 

@@ -9,7 +9,7 @@
 
 #include <hip/hip_runtime.h>
 
-#include "kernel_common.hpp"
+#include "../../ceres-solver-cuda_amd/csrc/kernel_common.hpp"
 
 namespace cse {
 
