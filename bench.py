@@ -35,9 +35,10 @@ same run (each with its own barrier-bracketed timing, max over ranks):
                  strips into pinned host memory (the reference's seam,
                  README.md:198-200; PCIe-inclusive, never `value`)
 and, on rank 0 at N=1, the CPU baseline (the oracle, oracle/, built
--O3 -march=native on this host) on every physical core of the affinity mask
-(the headline CPU leg, `speedup_vs_cpu`), at the box's CPU share and at 1
-thread, for residual+Jacobian and residual-only.
+-O3 -march=native on this host) on every physical core of the affinity mask,
+at the box's CPU share (the cgroup quota) and at 1 thread, for
+residual+Jacobian and residual-only; its value (and `speedup_vs_cpu`) is the
+fastest residual+Jacobian leg.
 
 Data is synthetic (no BAL file is available offline; see ceres_amd/bal.py for
 the generator), with the exact BAL header counts.  Rank 0 prints one JSON
@@ -103,9 +104,10 @@ def parse():
     ap.add_argument("--host-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the CPU baseline's headline leg; 0 = one per physical core "
-                         "of the affinity mask (a leg at the box's CPU share, $OMP_NUM_THREADS, "
-                         "and a 1-thread leg are timed beside it)")
+                    help="threads of the CPU baseline's all-core leg; 0 = one per physical core "
+                         "of the affinity mask (legs at the box's CPU share -- the cgroup quota, "
+                         "else $OMP_NUM_THREADS -- and at 1 thread are timed beside it; value = "
+                         "the fastest)")
     ap.add_argument("--seed", type=int, default=0xCE2E5)
     ap.add_argument("--lib", default=None, help="load this build of libcse.so (A/B runs)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -172,9 +174,35 @@ def _host_info():
         pass
     aff = os.sched_getaffinity(0)
     in_mask = {cpu_core[c] for c in aff if c in cpu_core}
+    quota, quota_src = _cpu_quota()
     return {"cpu_model": model, "logical_cpus": os.cpu_count(),
             "sockets": len({p for p, _ in phys}) or None, "physical_cores": len(phys) or None,
-            "affinity_cpus": len(aff), "physical_cores_in_affinity": len(in_mask) or len(aff)}
+            "affinity_cpus": len(aff), "physical_cores_in_affinity": len(in_mask) or len(aff),
+            "cgroup_cpu_quota": quota, "cgroup_cpu_quota_source": quota_src,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _cpu_quota():
+    """CPUs the cgroup's CFS quota grants this process (quota / period), or
+    None when unlimited or unreadable; and the file it came from."""
+    try:  # cgroup v2
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            return float(q) / float(per), "/sys/fs/cgroup/cpu.max"
+        return None, "/sys/fs/cgroup/cpu.max (max)"
+    except (OSError, ValueError):
+        pass
+    try:  # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        if q > 0:
+            return q / per, "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+        return None, "/sys/fs/cgroup/cpu/cpu.cfs_quota_us (-1)"
+    except (OSError, ValueError):
+        return None, None
 
 
 def _oracle_module():
@@ -196,10 +224,13 @@ def _oracle_module():
 def cpu_baseline(args, arrays, threads, share):
     """The oracle on bounded, point-bucket-aligned samples of the workload:
     residual+Jacobian and residual-only at `threads` (one per physical core
-    of the affinity mask: the all-core leg, `value`), at `share` (the box's
-    CPU share, $OMP_NUM_THREADS) and at 1 thread.  value = the all-core
-    residual+Jacobian rate in whole-workload evaluations per second (blocks
-    per second / the workload's blocks)."""
+    of the affinity mask), at `share` (the box's CPU share: the cgroup quota,
+    else $OMP_NUM_THREADS) and at 1 thread -- the reference's own benchmark
+    sweeps num_threads (evaluation_benchmark.cc:203-212).  value = the
+    FASTEST residual+Jacobian leg, in whole-workload evaluations per second
+    (blocks per second / the workload's blocks); `threads` = the thread count
+    that produced it, `cores` = the CPUs those threads could use (capped by
+    the cgroup quota)."""
     O, build = _oracle_module()
     cams, pts, ci, pi, obs = arrays
     total = len(ci)
@@ -241,15 +272,22 @@ def cpu_baseline(args, arrays, threads, share):
                 "evals_per_s": S / t / total, "blocks_per_s": S / t, "threads": nt,
                 "sample_blocks": S, "median_s": t}
             del r, j
-    head = legs[f"jacobian_{threads}t"]
-    return {"value": head["evals_per_s"], "unit": "evals/s", "cores": threads, "kind": "port",
-            "sample": (f"residual+Jacobian of all {total:,} residual blocks of the same workload "
-                       f"on {threads} threads (one per physical core of the affinity mask), "
-                       f"median of 3 after a warm-up; legs: the same at the box's CPU share "
-                       f"({share} threads), and 1-thread runs on the first 1/16 (Jacobian) or "
-                       f"1/8 (residual-only) of the blocks, cut at a point bucket; value = "
-                       f"blocks/s / {total:,}"),
-            "build": build, "host": _host_info(), "legs": legs}
+    host = _host_info()
+    best = max((v for k, v in legs.items() if k.startswith("jacobian_")),
+               key=lambda v: v["evals_per_s"])
+    quota = host["cgroup_cpu_quota"]
+    cores = best["threads"] if quota is None else max(1, min(best["threads"], int(round(quota))))
+    return {"value": best["evals_per_s"], "unit": "evals/s", "cores": cores,
+            "threads": best["threads"], "kind": "port",
+            "sample": (f"residual+Jacobian of all {total:,} residual blocks of the same workload, "
+                       f"median of 3 after a warm-up, at {sorted(set(counts))} threads "
+                       f"({threads} = one per physical core of the affinity mask, {share} = the "
+                       f"box's CPU share; 1-thread runs on the first 1/16 (Jacobian) or 1/8 "
+                       f"(residual-only) of the blocks, cut at a point bucket); value = the "
+                       f"fastest Jacobian leg ({best['threads']} threads), blocks/s / {total:,}; "
+                       f"cores = the CPUs that leg could use (cgroup quota "
+                       f"{quota if quota is not None else 'none'})"),
+            "build": build, "host": host, "legs": legs}
 
 
 # ---------------------------------------------------------------------------
@@ -552,7 +590,9 @@ def main():
         if arrays is not None:
             aff = len(os.sched_getaffinity(0))
             omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-            share = min(omp, aff) if omp > 0 else aff
+            quota, _ = _cpu_quota()
+            share = (max(1, min(int(quota), aff)) if quota is not None
+                     else min(omp, aff) if omp > 0 else aff)
             threads = args.cpu_threads or _host_info()["physical_cores_in_affinity"]
             cpu = cpu_baseline(args, arrays, threads, share)
         traffic = None

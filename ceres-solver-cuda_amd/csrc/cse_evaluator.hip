@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,6 +29,7 @@
 #ifdef CSE_TUNING
 #include "../../tools/tuning/persistent_launch.h"  // tuning build only
 #include "../../tools/tuning/pipeline_launch.h"    // tuning build only
+#include "../../tools/tuning/quad_kernel.hpp"      // tuning build only
 #endif
 
 namespace {
@@ -199,6 +201,8 @@ struct Group {
     // wave mode: chunks of at most cse::kGradChunk blocks
     DevBuf<int64_t> chunk_begin, chunk_off;
     DevBuf<int32_t> chunk_pb;  // parameter block (id) of each chunk
+    DevBuf<int32_t> chunk_order;  // passes > 1: the chunks pass-major (BuildGradPlan)
+    int passes = 1;
     DevBuf<double> chunk_partial;
     int64_t nchunks = 0;
     int64_t nperm = 0;  // blocks in the plan (all but those with a constant block)
@@ -321,6 +325,14 @@ template <class K, int L, int kStoreWaves, int kOpt = 0>
 void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
   cse::LaunchPipelinedSnavelyProbe<L, kStoreWaves, kOpt>(a, s);
+}
+
+// Tuning build: four-wave workgroups storing their four chunks' outputs as
+// long runs (tools/tuning/quad_kernel.hpp).  Variants 90, 91.
+template <class K, int L, int kSched>
+void LaunchQuad(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  hipLaunchKernelGGL((cse::EvaluateAffineQuad<K, L, kSched>), dim3((unsigned)num_wg),
+                     dim3(cse::kBlockThreads), 0, s, a);
 }
 
 // Tuning build: the BlockSparseMatrix Jacobian evaluation of the Snavely
@@ -547,6 +559,9 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 83: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 3>>;
     case 84: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 4>>;
     case 85: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 5>>;
+    // four-wave workgroups, long store runs (quad_kernel.hpp)
+    case 90: return &LaunchQuad<K, L, 0>;
+    case 91: return &LaunchQuad<K, L, 1>;
     default: return nullptr;
   }
 }
@@ -752,24 +767,57 @@ int Validate(const cse_problem_desc* d) {
 
 // Is the group table-free?  Returns the Policy (see evaluate_kernel.hpp
 // for the two affine shapes).
+// CameraGradientKernel's passes: its point gathers (slot 1, a table of
+// 8 s1 bytes per point) hit the Infinity Cache only while the table plus
+// every byte streamed between two uses of a line fits in ~256 MiB
+// (MI355X_MICROARCH.md, Infinity Cache).  In camera order a point's blocks
+// are spread over the whole launch, between which the sorted functor data
+// and slot-1 ids (8 data + 4 bytes a block) stream by: 107 + 580 MB at
+// problem-13682.  Cut into passes of consecutive point ranges, taken one
+// after the other, each pass touches 1/passes of both: passes = the total
+// over CSE_CAMGRAD_PASS_MB, at most 64.
+#ifndef CSE_CAMGRAD_PASS_MB
+#define CSE_CAMGRAD_PASS_MB 96
+#endif
+int CamGradPasses(const cse_residual_group& g, const KindShape& k) {
+  int32_t lo = INT32_MAX, hi = INT32_MIN;
+  for (int64_t i = 0; i < g.num_blocks; ++i) {
+    lo = std::min(lo, g.parameter_block_ids[i * k.nb + 1]);
+    hi = std::max(hi, g.parameter_block_ids[i * k.nb + 1]);
+  }
+  if (g.num_blocks == 0) return 1;
+  const double bytes = 8.0 * k.s1 * ((double)hi - lo + 1) + (8.0 * k.data + 4.0) * g.num_blocks;
+  const double per = (double)CSE_CAMGRAD_PASS_MB * 1e6;
+  const int p = (int)std::ceil(bytes / per);
+  return std::max(1, std::min(64, p));
+}
+
 // Blocks of slot j listed per parameter block (stable counting sort): the
 // gradient post-pass sums each parameter block's blocks in this order.
 // cpb (may be null): the descriptor's parameter blocks; blocks whose slot-j
 // parameter block is constant are left out (a held camera has no gradient
 // row), which makes the plan a permutation of the other blocks only.
+// passes > 1 (slot 0 of a two-slot kind): each parameter block's list is
+// further ordered by pass, pass(i) = i * passes / n (block order: in a
+// Schur-ordered problem, consecutive point ranges), and no chunk straddles
+// two passes; chunk_order lists the chunks pass-major, the order in which
+// CameraGradientKernel takes them (CamGradPasses).
 int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group::GradPlan* plan,
-                  hipStream_t s, const cse_parameter_block* cpb = nullptr) {
+                  hipStream_t s, const cse_parameter_block* cpb = nullptr, int passes = 1) {
   const int64_t n = g.num_blocks;
+  if (passes < 1 || n < passes) passes = 1;
   auto skip = [&](int64_t i) {
     return cpb && cpb[g.parameter_block_ids[i * k.nb + j]].is_constant;
   };
+  auto pass_of = [&](int64_t i) { return (int)((__int128)i * passes / n); };
   int32_t lo = g.parameter_block_ids[j], hi = lo;
   for (int64_t i = 0; i < n; ++i) {
     lo = std::min(lo, g.parameter_block_ids[i * k.nb + j]);
     hi = std::max(hi, g.parameter_block_ids[i * k.nb + j]);
   }
   const int64_t count = (int64_t)hi - lo + 1;
-  std::vector<int64_t> off(count + 1, 0);
+  // Counting sort on (parameter block, pass): poff[p * passes + t].
+  std::vector<int64_t> poff(count * passes + 1, 0);
   bool sorted = true;
   int64_t kept = 0, prev = INT64_MIN;
   for (int64_t i = 0; i < n; ++i) {
@@ -778,19 +826,22 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
       continue;
     }
     const int32_t id = g.parameter_block_ids[i * k.nb + j];
-    ++off[id - lo + 1];
+    ++poff[(id - lo) * passes + pass_of(i) + 1];
     if (id < prev) sorted = false;
     prev = id;
     ++kept;
   }
   plan->nperm = kept;
-  for (int64_t p = 0; p < count; ++p) off[p + 1] += off[p];
+  for (int64_t p = 0; p < count * passes; ++p) poff[p + 1] += poff[p];
+  std::vector<int64_t> off(count + 1);
+  for (int64_t p = 0; p <= count; ++p) off[p] = poff[p * passes];
   int rc;
   if (!sorted) {
     std::vector<int32_t> perm(std::max<int64_t>(kept, 1));
-    std::vector<int64_t> next(off.begin(), off.end() - 1);
+    std::vector<int64_t> next(poff.begin(), poff.end() - 1);
     for (int64_t i = 0; i < n; ++i)
-      if (!skip(i)) perm[next[g.parameter_block_ids[i * k.nb + j] - lo]++] = (int32_t)i;
+      if (!skip(i))
+        perm[next[(g.parameter_block_ids[i * k.nb + j] - lo) * passes + pass_of(i)]++] = (int32_t)i;
     if ((rc = plan->perm.upload(perm.data(), perm.size(), s))) return rc;
     if (hipStreamSynchronize(s) != hipSuccess) return Fail(CSE_ERR_HIP, "hipStreamSynchronize failed");
   }
@@ -802,16 +853,27 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
   // Chunks: the wave-mode post-pass and the fused gradient's slot-0 pass.
   if (!sorted) {
     std::vector<int64_t> begin, coff(count + 1, 0);
-    std::vector<int32_t> cpb;
+    std::vector<int32_t> cpb, cpass;
     for (int64_t p = 0; p < count; ++p) {
       coff[p] = (int64_t)begin.size();
-      for (int64_t q = off[p]; q < off[p + 1]; q += cse::kGradChunk) {
-        begin.push_back(q);
-        cpb.push_back((int32_t)(lo + p));
-      }
+      for (int t = 0; t < passes; ++t)
+        for (int64_t q = poff[p * passes + t]; q < poff[p * passes + t + 1]; q += cse::kGradChunk) {
+          begin.push_back(q);
+          cpb.push_back((int32_t)(lo + p));
+          cpass.push_back(t);
+        }
     }
     coff[count] = (int64_t)begin.size();
     plan->nchunks = (int64_t)begin.size();
+    plan->passes = passes;
+    if (passes > 1) {  // pass-major launch order, camera order within a pass
+      std::vector<int32_t> order;
+      order.reserve(begin.size());
+      for (int t = 0; t < passes; ++t)
+        for (int64_t c = 0; c < plan->nchunks; ++c)
+          if (cpass[c] == t) order.push_back((int32_t)c);
+      if ((rc = plan->chunk_order.upload(order.data(), order.size(), s))) return rc;
+    }
     // Chunk c covers [begin[c], begin[c + 1]): a parameter block's last
     // chunk ends at off[p + 1], where the next non-empty one starts.
     begin.push_back(kept);
@@ -1195,6 +1257,7 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
   cg.sid1 = G.sid1.p;
   cg.chunk_pb = P.chunk_pb.p;
   cg.chunk_begin = P.chunk_begin.p;
+  cg.chunk_order = P.chunk_order.p;
   cg.partial = P.chunk_partial.p;
   cg.nchunks = P.nchunks;
   cg.loss.a = G.loss.a;
@@ -1775,7 +1838,8 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       for (int j = 0; j < k.nb; ++j)
         if (GradSupported(k.nr, sizes[j]) &&
             (rc = BuildGradPlan(g, k, j, &G.grad[j], s,
-                                j == 0 && G.const0 ? d->parameter_blocks : nullptr)))
+                                j == 0 && G.const0 ? d->parameter_blocks : nullptr,
+                                j == 0 && k.nb == 2 ? CamGradPasses(g, k) : 1)))
           return bail(rc);
     }
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);

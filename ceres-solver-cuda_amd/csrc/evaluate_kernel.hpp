@@ -1562,6 +1562,7 @@ struct CamGradArgs {
   const int32_t* sid1;         // [n] slot-1 ids, same order
   const int32_t* chunk_pb;     // [nchunks] slot-0 id of each chunk
   const int64_t* chunk_begin;  // [nchunks + 1]
+  const int32_t* chunk_order;  // [nchunks] the order to take them in (null: 0, 1, ...)
   double* partial;             // [nchunks][S0]
   int64_t nchunks;
   LossParams loss;
@@ -1608,6 +1609,11 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
   }
 }
 
+// The sorted slot-1 ids streamed non-temporally (1) or with the default
+// policy (0), like the functor data.
+#ifndef CSE_CAMGRAD_NT_IDS
+#define CSE_CAMGRAD_NT_IDS 0
+#endif
 // CSE_CAMGRAD_WAVES: a lower bound on its waves per SIMD (A/B builds; 1 = the
 // compiler's choice, 158 VGPRs = 3 with the by-hand functor).
 #ifndef CSE_CAMGRAD_WAVES
@@ -1621,8 +1627,11 @@ CameraGradientKernel(const CamGradArgs g) {
   static_assert(Tr::NB == 2 && S1 > 0, "two-slot kinds");
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = kWPB == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int64_t cid = (int64_t)blockIdx.x * kWPB + wave;
-  if (cid >= g.nchunks) return;
+  const int64_t slot = (int64_t)blockIdx.x * kWPB + wave;
+  if (slot >= g.nchunks) return;
+  // Pass-major (BuildGradPlan): the resident waves gather from one point
+  // range at a time, small enough to stay in the Infinity Cache.
+  const int64_t cid = g.chunk_order ? (int64_t)g.chunk_order[slot] : slot;
   const int64_t q0 = g.chunk_begin[cid], q1 = g.chunk_begin[cid + 1];
   constexpr int X0 = Tr::X0;
   const double* cam = g.packed0 ? g.packed0 + (int64_t)g.packed_stride * (g.chunk_pb[cid] - g.packed_lo)
@@ -1650,9 +1659,10 @@ CameraGradientKernel(const CamGradArgs g) {
     for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int k = 0; k < D; ++k) d[u][k] = __builtin_nontemporal_load(g.sdata + qb[u] * D + k);
+      const int32_t id1 = CSE_CAMGRAD_NT_IDS ? __builtin_nontemporal_load(g.sid1 + qb[u]) : g.sid1[qb[u]];
       if constexpr (S1 == 3) {
         if (g.ppad) {  // the 32-byte-stride copy: one sector per point
-          const double* p1 = g.ppad + 4LL * (g.sid1[qb[u]] - g.ppad_lo);
+          const double* p1 = g.ppad + 4LL * (id1 - g.ppad_lo);
           const double2 xy = *reinterpret_cast<const double2*>(p1);
           x1[u][0] = xy.x;
           x1[u][1] = xy.y;
@@ -1660,7 +1670,7 @@ CameraGradientKernel(const CamGradArgs g) {
           continue;
         }
       }
-      const double* p1 = g.state + g.state_base1 + (int64_t)S1 * g.sid1[qb[u]];
+      const double* p1 = g.state + g.state_base1 + (int64_t)S1 * id1;
 #pragma unroll
       for (int k = 0; k < S1; ++k) x1[u][k] = p1[k];
     }
