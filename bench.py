@@ -31,6 +31,8 @@ same run (each with its own barrier-bracketed timing, max over ranks):
                  (CSE_EVAL_SAME_POINT: the Jacobian at a just-accepted
                  candidate, trust_region_minimizer.cc:822-826; no repack)
   residual_only  residuals + cost (trust_region_minimizer.cc:770-788)
+  jet            the headline evaluation with the Jacobian by Jet<double, 12>
+                 (cse_options.jacobian_form; the headline uses the closed form)
   host_strips    evaluation + D2H of each rank's residual and Jacobian
                  strips into pinned host memory (the reference's seam,
                  README.md:198-200; PCIe-inclusive, never `value`)
@@ -526,6 +528,36 @@ def main():
                     "headline value)"}
         del hres, hjac
 
+        if world == 1 and not variant:
+            # The same evaluation with the Jacobian by forward-mode
+            # Jet<double, 12> (cse_options.jacobian_form = CSE_JACOBIAN_JET),
+            # as AutoDifferentiate computes it for any AutoDiffCostFunction
+            # (autodiff.h:314-381): its own evaluator over the same program,
+            # writing the headline's buffers.
+            jev = ca.Evaluator(prog, device=dev_index, profile=True, stream=stream.cuda_stream,
+                               jacobian_form="jet")
+            saved = se, ev
+            st_, cost_, res_, jac_ = se.state, se.cost, se.residuals, se.jacobian
+
+            class _JetLeg:  # what run_leg needs of `se`
+                def wait_exchange(self):
+                    pass
+
+                def wait(self):
+                    return jev.wait()
+
+            se, ev = _JetLeg(), jev
+            try:
+                leg("jet", lambda: jev.evaluate_device(st_.data_ptr(), cost_.data_ptr(), res_.data_ptr(),
+                                                       None, jac_.data_ptr()),
+                    info.bytes_jacobian_eval, ks,
+                    "the headline evaluation with the Jacobian by forward-mode Jet<double, 12> "
+                    "(cse_options.jacobian_form = CSE_JACOBIAN_JET; AutoDifferentiate, "
+                    "autodiff.h:314-381) instead of the closed-form Snavely Jacobian: "
+                    "EvaluateAffineChunksTwoRoundW1<SnavelyJetKind, ...>")
+            finally:
+                se, ev = saved
+                jev.close()
         if world == 1 and args.config == "problem-13682-4456117" and not variant:
             # BASELINE.json configs[2] (problem-1778, HuberLoss,
             # CompressedRowSparseMatrix) in the same driver-timed run: its own

@@ -12,7 +12,11 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libcse.so"))
 
-CSE_ABI_VERSION = 2
+CSE_ABI_VERSION = 3
+
+# cse_options.jacobian_form (cse_jacobian_form)
+JACOBIAN_CLOSED_FORM = 0
+JACOBIAN_JET = 1
 CSE_OK = 0
 CSE_EVALUATION_FAILED = 1
 CSE_ERR_INVALID = -1
@@ -110,7 +114,7 @@ class cse_options(C.Structure):
     _fields_ = [("device", C.c_int32), ("check_finite", C.c_int32),
                 ("apply_loss_function", C.c_int32), ("force_general_layout", C.c_int32),
                 ("profile", C.c_int32), ("use_stream", C.c_int32), ("stream", C.c_void_p),
-                ("gradient_mode", C.c_int32)]
+                ("gradient_mode", C.c_int32), ("jacobian_form", C.c_int32)]
 
 
 class cse_info(C.Structure):

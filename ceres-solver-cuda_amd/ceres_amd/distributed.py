@@ -34,7 +34,8 @@ class ShardedEvaluator:
 
     def __init__(self, cameras, points, cam_idx, pt_idx, obs, rank, world, device, loss=None,
                  format=BLOCK_SPARSE, gradient=False, gradient_mode=0, stream=None, group=None,
-                 quaternion_manifold=False, constant_cameras=()):
+                 quaternion_manifold=False, constant_cameras=(), jacobian_form="closed",
+                 exchange=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -54,7 +55,8 @@ class ShardedEvaluator:
             stream = torch.cuda.current_stream(self.device)
         self.stream = stream
         self.evaluator = Evaluator(self.program, device=device, profile=True,
-                                   stream=stream.cuda_stream, gradient_mode=gradient_mode)
+                                   stream=stream.cuda_stream, gradient_mode=gradient_mode,
+                                   jacobian_form=jacobian_form)
         p = self.program
         f64 = torch.float64
         dev = self.device
@@ -70,9 +72,15 @@ class ShardedEvaluator:
         self._cam_rows = (3 * npts, 3 * npts + self.cam_size * self.num_cameras)
         # The exchange runs whenever the process group has several ranks
         # (also for replica shards, world == 1 here).  gloo reduces host
-        # tensors; RCCL reduces in place in HBM.
-        self.exchange = (dist.is_available() and dist.is_initialized()
-                         and dist.get_world_size(group) > 1)
+        # tensors; RCCL reduces in place in HBM.  exchange=True forces it on a
+        # one-rank group (the RCCL path on a one-GPU box), False switches it off.
+        grouped = dist.is_available() and dist.is_initialized()
+        if exchange is None:
+            self.exchange = grouped and dist.get_world_size(group) > 1
+        else:
+            if exchange and not grouped:
+                raise ValueError("exchange=True needs an initialised process group")
+            self.exchange = bool(exchange)
         self._host_reduce = self.exchange and dist.get_backend(group) == "gloo"
         self._pending = []
 

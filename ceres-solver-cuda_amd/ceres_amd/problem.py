@@ -408,20 +408,37 @@ class ProblemCUDA:
         return prog
 
 
+# Arrays registered by host_register, by buffer address: the module keeps
+# each one alive until host_unregister, so a registered address is never
+# freed (and reused) while the library's registry still lists it.
+_registered = {}
+
+
 def host_register(arr):
-    """Page-lock a C-contiguous numpy array for asynchronous transfers
-    (cse_host_register) until host_unregister(arr); the multi-device
-    evaluator copies into and out of such buffers without staging.  Keep the
-    array alive while registered."""
-    arr = np.asarray(arr)
+    """Page-lock a C-contiguous numpy array in place for asynchronous
+    transfers (cse_host_register) until host_unregister(arr); the
+    multi-device evaluator copies into and out of such buffers without
+    staging.  Only an existing ndarray is accepted (no conversion, so it is
+    the caller's own buffer that is registered); the module holds a
+    reference to it until it is unregistered."""
+    if not isinstance(arr, np.ndarray):
+        raise TypeError("host_register: a numpy.ndarray (registered in place, never a copy)")
     if not arr.flags.c_contiguous or arr.nbytes == 0:
         raise ValueError("host_register: a non-empty C-contiguous array")
-    _cse.check(_cse.lib().cse_host_register(arr.ctypes.data, arr.nbytes), "cse_host_register")
+    addr = arr.ctypes.data
+    if addr in _registered:
+        raise ValueError("host_register: this buffer is already registered")
+    _cse.check(_cse.lib().cse_host_register(addr, arr.nbytes), "cse_host_register")
+    _registered[addr] = arr
     return arr
 
 
 def host_unregister(arr):
-    _cse.check(_cse.lib().cse_host_unregister(np.asarray(arr).ctypes.data), "cse_host_unregister")
+    if not isinstance(arr, np.ndarray) or arr.ctypes.data not in _registered:
+        raise ValueError("host_unregister: not an array registered by host_register")
+    addr = arr.ctypes.data
+    _cse.check(_cse.lib().cse_host_unregister(addr), "cse_host_unregister")
+    del _registered[addr]
 
 
 class Evaluator:
@@ -429,11 +446,14 @@ class Evaluator:
 
     def __init__(self, program, device=-1, check_finite=True, apply_loss_function=True,
                  force_general_layout=False, profile=False, stream=None, gradient_mode=0,
-                 devices=None):
+                 devices=None, jacobian_form="closed"):
         """devices: a list of HIP ordinals -> one evaluator over several
         devices (cse_create_multi: point-bucket shards, strips copied into
         the caller's one host buffer); repeats put several shards on one
-        device.  Only the host-pointer calls work on it."""
+        device.  Only the host-pointer calls work on it.
+        jacobian_form: "closed" (the Snavely functor's closed-form Jacobian,
+        the default) or "jet" (forward-mode Jet<double, 12>, as
+        AutoDifferentiate; cse_options.jacobian_form)."""
         self.program = program
         self.desc = program.descriptor()
         opts = _cse.cse_options()
@@ -446,6 +466,10 @@ class Evaluator:
         opts.profile = int(profile)
         # 0 = fused where eligible (else 1), 1 = post-pass, 2 = atomics (cse.h)
         opts.gradient_mode = int(gradient_mode)
+        forms = {"closed": _cse.JACOBIAN_CLOSED_FORM, "jet": _cse.JACOBIAN_JET}
+        if jacobian_form not in forms:
+            raise ValueError(f"jacobian_form must be one of {sorted(forms)}")
+        opts.jacobian_form = forms[jacobian_form]
         # stream: a hipStream_t handle (int) to run on -- 0 is the null stream
         # (torch's default stream); None = an evaluator-owned stream.
         opts.use_stream = int(stream is not None)

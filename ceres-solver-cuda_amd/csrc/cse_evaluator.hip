@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/cse.h"
+#include "jet_kernels.h"
 #include "multi_device.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
@@ -223,6 +224,9 @@ struct Group {
   // boundary entries and slot-0 contributions (allocated on first use).
   bool fuse_ok = false;
   DevBuf<double> gside, gcontrib;
+  // cse_options.jacobian_form = CSE_JACOBIAN_JET on a Snavely group: its
+  // Jacobian kernels are the Jet<double, 12> instantiations (jet_kernels.h).
+  bool jet = false;
   // Slot-0-sorted functor data and slot-1 ids (CameraGradientKernel; built
   // on first use).
   DevBuf<double> sdata;
@@ -1292,7 +1296,8 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
                              dim3(W * cse::kWave), 0, s, cg);
       }
     };
-    if (G.kind == kKindQuaternionTangent) launch(cse::SnavelyQuaternionTangentKind{});
+    if (G.jet) cse::LaunchJetCameraGradient(G.loss.kind, cg, P.nchunks, s);
+    else if (G.kind == kKindQuaternionTangent) launch(cse::SnavelyQuaternionTangentKind{});
     else launch(cse::SnavelyKind{});
   }
   CSE_HIP(hipGetLastError());
@@ -1454,6 +1459,9 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     if (G.n == 0) continue;
     const bool dma = G.packed0.p != nullptr;
     LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma, G.const0);
+    if (G.jet && jets)  // the Jet<double, 12> instantiations (cse_create kept only these shapes)
+      fn = G.policy == kTable ? cse::JetSnavelyTable(G.loss.kind)
+                              : cse::JetSnavelyJacobian(G.loss.kind, G.policy == kAffineCrs);
     if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
     // Gradient: a deterministic post-pass over the written residuals and
     // Jacobian when the group has plans for all its slots, else in-kernel
@@ -1463,7 +1471,10 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     const int mode = ev->opts.gradient_mode;
     // Mode 1 (post-pass) has no form over the packed F cells of a group with
     // constant slot-0 blocks: it takes mode 0's fused form (also fixed order).
-    const bool fused = grad_pass && G.fuse_ok && (mode == 0 || mode == 3 || (mode == 1 && G.const0));
+    // The Jet form has no mode-3 kernel (contributions in block order): the
+    // post-pass instead, as for groups without a fused form.
+    const bool fused = grad_pass && G.fuse_ok &&
+                       (mode == 0 || (mode == 3 && !G.jet) || (mode == 1 && G.const0));
     // Constant slot-0 blocks: no post-pass over the packed F cells (in-kernel
     // atomics instead, active cameras only).
     if (G.const0 && !fused) grad_pass = false;
@@ -1483,6 +1494,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
         a.ppad_lo = G.grad[1].lo;
       }
       fn = PickFused(G.kind, G.loss.kind, G.policy, recompute, G.const0);
+      if (G.jet) fn = cse::JetSnavelyFusedPoints(G.loss.kind, G.policy == kAffineCrs);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
     if (dma && repack) {
@@ -1516,10 +1528,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       // The 64-byte sectors two held-camera chunks share (the full chunks
       // stored their heads and tails in side slots), when the full chunks
       // took that tail: the same base alignment test as the kernel.
-      const uintptr_t m = (d_res ? reinterpret_cast<uintptr_t>(d_res + G.res_base) : 0) |
-                          reinterpret_cast<uintptr_t>(d_jac + G.jac_base[1][0]) |
-                          reinterpret_cast<uintptr_t>(d_jac + G.h_fbase[0]);
-      if ((m & 15) == 0) {
+      if (cse::HeldWindowsAligned(d_res, G.res_base, d_jac, G.jac_base[1][0], G.h_fbase[0])) {
         const int64_t nchunks = (G.n + cse::kWave - 1) / cse::kWave;
         const int64_t threads = 4 * nchunks;
         hipLaunchKernelGGL(cse::HeldSectorFixupKernel,
@@ -1622,6 +1631,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   if (ev->opts.gradient_mode < 0 || ev->opts.gradient_mode > 3)
     return bail(Fail(CSE_ERR_INVALID, "gradient_mode " + std::to_string(ev->opts.gradient_mode) +
                                           " is not one of 0..3"));
+  if (ev->opts.jacobian_form != CSE_JACOBIAN_CLOSED_FORM && ev->opts.jacobian_form != CSE_JACOBIAN_JET)
+    return bail(Fail(CSE_ERR_INVALID, "jacobian_form " + std::to_string(ev->opts.jacobian_form) +
+                                          " is not a cse_jacobian_form"));
 
   if (ev->opts.device >= 0) {
     const hipError_t e = hipSetDevice(ev->opts.device);
@@ -1769,6 +1781,16 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
         G.kind = g.functor_kind;
         ShapeOf(G.kind, &G.shape);
       }
+    }
+    // The Jet form of the Snavely functor (cse_options.jacobian_form) is
+    // instantiated for the affine kernels with the LDS-DMA gather and without
+    // held cameras, and for the table kernel: other Snavely groups take the
+    // table path.
+    G.jet = ev->opts.jacobian_form == CSE_JACOBIAN_JET && g.functor_kind == CSE_FUNCTOR_SNAVELY_2_9_3;
+    if (G.jet && G.affine && (G.const0 || G.slot0_count <= 0 || G.slot0_count > (1 << 20))) {
+      G.policy = kTable;
+      G.affine = false;
+      G.const0 = false;
     }
     // Table-path tables: also for const0 groups (their J products use the
     // table kernels).
@@ -2469,7 +2491,7 @@ int cse_get_info(cse_evaluator* ev, cse_info* info) {
   for (auto& G : ev->groups) {
     info->num_affine_groups += G.affine ? 1 : 0;
     info->num_fused_gradient_groups +=
-        (G.fuse_ok && (ev->opts.gradient_mode == 0 || ev->opts.gradient_mode == 3 ||
+        (G.fuse_ok && (ev->opts.gradient_mode == 0 || (ev->opts.gradient_mode == 3 && !G.jet) ||
                        (ev->opts.gradient_mode == 1 && G.const0)))
             ? 1
             : 0;

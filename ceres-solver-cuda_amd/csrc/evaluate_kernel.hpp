@@ -581,13 +581,19 @@ __device__ __forceinline__ void ReadSegmentPiecesRange(const double* staged, int
 // tail?  The residual, E-cell and F-cell bases 16-byte aligned (the chunk
 // segments then start on 64-byte sectors when the bases do).
 // fb_first: a.fbase[0].
-__device__ __forceinline__ bool C0Aligned(const GroupArgs& a, int64_t fb_first) {
+// The one test, on the host (whether HeldSectorFixupKernel must run after
+// the kernel, cse_evaluator.hip) and in the kernel (whether full chunks take
+// the sector-window tail), so the two can never disagree.
+CSE_HD bool HeldWindowsAligned(const double* residuals, int64_t res_base, const double* jacobian,
+                                      int64_t e_base, int64_t f_first) {
   uintptr_t m = 0;
-  if (a.residuals) m |= reinterpret_cast<uintptr_t>(a.residuals + a.res_base);
-  if (a.jacobian)
-    m |= reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[1][0]) |
-         reinterpret_cast<uintptr_t>(a.jacobian + fb_first);
+  if (residuals) m |= reinterpret_cast<uintptr_t>(residuals + res_base);
+  if (jacobian)
+    m |= reinterpret_cast<uintptr_t>(jacobian + e_base) | reinterpret_cast<uintptr_t>(jacobian + f_first);
   return (m & 15) == 0;
+}
+__device__ __forceinline__ bool C0Aligned(const GroupArgs& a, int64_t fb_first) {
+  return HeldWindowsAligned(a.residuals, a.res_base, a.jacobian, a.jac_base[1][0], fb_first);
 }
 
 // Pieces kJ.. of a wave segment as SegmentStoresFrom, lane `lane` of

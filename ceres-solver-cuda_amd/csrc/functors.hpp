@@ -183,6 +183,14 @@ struct SnavelyKind {
   CSE_FLAT_FROM_TWO_SLOTS
 };
 
+// The same functor with its Jacobian by forward-mode Jet<double, 12>, as
+// AutoDifferentiate computes it (include/ceres/internal/autodiff.h:314-381;
+// AutoDiffCostFunction, autodiff_cost_function_cuda.h:55-71), instead of
+// SnavelyJacobianByHand: cse_options.jacobian_form = CSE_JACOBIAN_JET.  A
+// distinct type so that the kernels' by-hand dispatch (is_same<K,
+// SnavelyKind>) passes it by; instantiated in its own TU (jet_kernels.hip).
+struct SnavelyJetKind : SnavelyKind {};
+
 // SnavelyReprojectionError's residuals and Jacobian blocks written out by
 // hand (the product rule the seeded Jet<12> applies, collected into 3x3
 // matrices): J0 = dr/d[aa, t, f, l1, l2] (2 x 9), J1 = dr/dX (2 x 3), both

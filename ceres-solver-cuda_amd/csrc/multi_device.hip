@@ -128,6 +128,13 @@ struct CseMulti {
     // Jacobian values (the strips).
     std::vector<Interval> state_iv, res_iv, jac_iv, grad_iv;
     int64_t nstate = 0, nres = 0, njac = 0, ngrad = 0;
+    // The plus-Jacobian values of the shard's parameter blocks, compacted
+    // (global -> local intervals of the caller's plus_jacobians array).
+    std::vector<Interval> pj_iv;
+    int64_t npj = 0;
+    // Pinned staging of the shard's state slices (allocated on first use):
+    // one H2D copy per evaluation however many intervals the slices form.
+    double* h_state = nullptr;
     double *d_state = nullptr, *d_cost = nullptr, *d_res = nullptr, *d_jac = nullptr,
            *d_grad = nullptr;
     double *h_cost = nullptr, *h_grad = nullptr;  // pinned
@@ -151,7 +158,7 @@ void ReleaseShard(CseMulti::Shard& s) {
   (void)hipSetDevice(s.device);
   for (double* p : {s.d_state, s.d_cost, s.d_res, s.d_jac, s.d_grad})
     if (p) (void)hipFree(p);
-  for (double* p : {s.h_cost, s.h_grad, s.h_x, s.h_d, s.h_o})
+  for (double* p : {s.h_cost, s.h_grad, s.h_x, s.h_d, s.h_o, s.h_state})
     if (p) (void)hipHostFree(p);
   if (s.stream) (void)hipStreamDestroy(s.stream);
   s = CseMulti::Shard{};
@@ -174,7 +181,10 @@ bool RuntimePinned(const void* p) {
 }
 
 // May [p, p + bytes) take asynchronous copies?  Inside one cse_host_register
-// range, or pinned by the caller at both ends.
+// range, or inside ONE page-locked allocation of the caller's (hipHostMalloc
+// or hipHostRegister): the runtime's address range of p must cover the
+// whole buffer (a range over two pinned allocations with pageable memory
+// between them is not pinned).
 bool Pinned(const void* p, size_t bytes) {
   if (!p || bytes == 0) return false;
   const uintptr_t b = reinterpret_cast<uintptr_t>(p), e = b + bytes;
@@ -183,7 +193,18 @@ bool Pinned(const void* p, size_t bytes) {
     for (const auto& r : g_reg)
       if (b >= r.first && e <= r.second) return true;
   }
-  return RuntimePinned(p) && RuntimePinned(static_cast<const char*>(p) + bytes - 1);
+  if (!RuntimePinned(p)) return false;
+  void* start = nullptr;
+  size_t size = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t rb = reinterpret_cast<uintptr_t>(start);
+  return rb <= b && e <= rb + size;
 }
 
 // Cut positions in the global residual-block index (module comment).
@@ -239,11 +260,26 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
     }
     s.nstate = IntervalsOf(st, &s.state_iv);
     s.ngrad = IntervalsOf(dl, &s.grad_iv);
+    std::vector<std::pair<int64_t, int64_t>> pj;
+    for (const auto& pb : pbs)
+      if (pb.plus_jacobian_offset >= 0)
+        pj.push_back({pb.plus_jacobian_offset,
+                      pb.plus_jacobian_offset + (int64_t)pb.size * pb.tangent_size});
+    s.npj = IntervalsOf(pj, &s.pj_iv);
     for (auto& pb : pbs) {
+      if (pb.plus_jacobian_offset >= 0) pb.plus_jacobian_offset = LocalOf(s.pj_iv, pb.plus_jacobian_offset);
       if (pb.is_constant) continue;  // offsets into the (whole) constant state
       pb.state_offset = LocalOf(s.state_iv, pb.state_offset);
       if (pb.tangent_size > 0) pb.delta_offset = LocalOf(s.grad_iv, pb.delta_offset);
     }
+  }
+  // The shard's plus-Jacobian values only (cse_set_plus_jacobians refreshes
+  // them through the same intervals).
+  std::vector<double> pj_local;
+  if (s.npj > 0 && d->plus_jacobians) {
+    pj_local.resize((size_t)s.npj);
+    for (const auto& iv : s.pj_iv)
+      std::copy(d->plus_jacobians + iv.begin, d->plus_jacobians + iv.end, pj_local.begin() + iv.local);
   }
   // Groups restricted to the shard, renumbered from g0, ids mapped to the
   // shard's parameter blocks.
@@ -365,6 +401,8 @@ int CreateShard(const cse_problem_desc* d, const cse_options* opts, CseMulti::Sh
                                                 : nullptr;
   sd.num_jacobian_per_residual_offsets = (int64_t)jac_offsets.size();
   sd.num_jacobian_values = s.njac;
+  sd.num_plus_jacobian_values = s.npj;
+  sd.plus_jacobians = s.npj > 0 ? pj_local.data() : nullptr;
   // Device, stream, buffers, then the shard's evaluator on that stream.
   MD_HIP(hipSetDevice(s.device));
   MD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
@@ -497,6 +535,10 @@ void Drain(CseMulti* m, size_t upto) {
 
 }  // namespace
 
+// A page-locked caller state is copied slice by slice while it has at most
+// this many slices; beyond, through the shard's staging in one copy.
+constexpr size_t kDirectStateIntervals = 8;
+
 int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residuals,
                   double* gradient, double* jac, bool same_point) {
   if (jac && !m->has_layout)
@@ -513,15 +555,23 @@ int MultiEvaluate(CseMulti* m, const double* state, double* cost, double* residu
 #define MD_Q(call)                                                                         do {                                                                                       hipError_t e_ = (call);                                                                  if (e_ != hipSuccess) {                                                                    Drain(m, queued + 1);                                                                    return CseFail(CSE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));        }                                                                                      } while (0)
   for (auto& s : m->shards) {
     MD_Q(hipSetDevice(s.device));
-    if (copy_state)
-      for (const auto& iv : s.state_iv) {
-        const size_t bytes = (iv.end - iv.begin) * sizeof(double);
-        if (async_state)
-          MD_Q(hipMemcpyAsync(s.d_state + iv.local, state + iv.begin, bytes, hipMemcpyHostToDevice,
-                              s.stream));
-        else
-          MD_Q(hipMemcpy(s.d_state + iv.local, state + iv.begin, bytes, hipMemcpyHostToDevice));
+    if (copy_state && s.nstate > 0) {
+      if (async_state && s.state_iv.size() <= kDirectStateIntervals) {
+        for (const auto& iv : s.state_iv)
+          MD_Q(hipMemcpyAsync(s.d_state + iv.local, state + iv.begin, (iv.end - iv.begin) * sizeof(double),
+                              hipMemcpyHostToDevice, s.stream));
+      } else {
+        // Many slices (a BAL shard's cameras), or pageable state: gathered on
+        // the host into the shard's pinned staging, then one copy.  The
+        // staging is free again: the previous call waited for every shard.
+        if (!s.h_state)
+          MD_Q(hipHostMalloc(reinterpret_cast<void**>(&s.h_state), s.nstate * sizeof(double)));
+        for (const auto& iv : s.state_iv)
+          std::memcpy(s.h_state + iv.local, state + iv.begin, (iv.end - iv.begin) * sizeof(double));
+        MD_Q(hipMemcpyAsync(s.d_state, s.h_state, s.nstate * sizeof(double), hipMemcpyHostToDevice,
+                            s.stream));
       }
+    }
     int rc = cse_evaluate_device_ex(s.ev, s.d_state, s.d_cost, residuals ? s.d_res : nullptr,
                                     gradient ? s.d_grad : nullptr, jac ? s.d_jac : nullptr,
                                     same_point ? CSE_EVAL_SAME_POINT : 0u);
@@ -637,8 +687,13 @@ int MultiShardInfo(CseMulti* m, int32_t* num_shards, int64_t* first_block, int32
 }
 
 int MultiSetPlusJacobians(CseMulti* m, const double* pj) {
+  std::vector<double> local;
   for (auto& s : m->shards) {
-    const int rc = cse_set_plus_jacobians(s.ev, pj);
+    if (s.npj == 0) continue;
+    if (!pj) return CseFail(CSE_ERR_INVALID, "null plus_jacobians");
+    local.resize((size_t)s.npj);
+    for (const auto& iv : s.pj_iv) std::copy(pj + iv.begin, pj + iv.end, local.begin() + iv.local);
+    const int rc = cse_set_plus_jacobians(s.ev, local.data());
     if (rc) return rc;
   }
   return CSE_OK;
@@ -649,6 +704,9 @@ int MultiPlus(CseMulti* m, const double* state, const double* delta, double* out
   // by several shards gets the same result from each); every active block
   // belongs to some shard (MultiCreate).  Local slices through pinned
   // staging, the shard's own cse_plus in between.
+  // Every shard's inputs are gathered before any output is written, so `out`
+  // may alias `state` (in-place Plus, as Program::Plus allows): a camera
+  // held by two shards is read once, before either writes it.
   for (auto& s : m->shards) {
     if (s.nstate == 0) continue;
     MD_HIP(hipSetDevice(s.device));
@@ -660,8 +718,15 @@ int MultiPlus(CseMulti* m, const double* state, const double* delta, double* out
       std::memcpy(s.h_x + iv.local, state + iv.begin, (iv.end - iv.begin) * sizeof(double));
     for (const auto& iv : s.grad_iv)
       std::memcpy(s.h_d + iv.local, delta + iv.begin, (iv.end - iv.begin) * sizeof(double));
+  }
+  for (auto& s : m->shards) {
+    if (s.nstate == 0) continue;
+    MD_HIP(hipSetDevice(s.device));
     const int rc = cse_plus(s.ev, s.h_x, s.h_d, s.h_o);
     if (rc) return rc;
+  }
+  for (auto& s : m->shards) {
+    if (s.nstate == 0) continue;
     for (const auto& iv : s.state_iv)
       std::memcpy(out + iv.begin, s.h_o + iv.local, (iv.end - iv.begin) * sizeof(double));
   }

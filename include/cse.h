@@ -28,8 +28,9 @@ extern "C" {
 
 /* 2: cse_parameter_block.manifold (was `reserved`, which had to be 0),
  *    cse_host_register / cse_host_unregister, cse_shard_transfer_bytes,
- *    shard-local state in cse_create_multi. */
-#define CSE_ABI_VERSION 2
+ *    shard-local state in cse_create_multi.
+ * 3: cse_options.jacobian_form. */
+#define CSE_ABI_VERSION 3
 
 /* Return codes. */
 #define CSE_OK 0
@@ -198,8 +199,25 @@ typedef struct cse_options {
                                    as cuda_evaluator_kernel.h:149-160; 3 = fused,
                                    slot-0 contributions written in block order and
                                    summed per block (the round-2 form), else 1.
-                                   0, 1 and 3 are bit-deterministic. */
+                                   0, 1 and 3 are bit-deterministic.  With
+                                   jacobian_form CSE_JACOBIAN_JET, 3 runs as 1. */
+  int32_t jacobian_form;        /* cse_jacobian_form: how the SnavelyReprojectionError
+                                   Jacobian is differentiated (every other kind always
+                                   uses Jet<double, N>, AutoDifferentiate) */
 } cse_options;
+
+/* cse_options.jacobian_form.  Both give the Jacobian of the same functor to
+ * within the parity bounds; the closed form is faster (fewer FP64 operations,
+ * fewer registers). */
+typedef enum cse_jacobian_form {
+  /* Snavely<2,9,3>: the forward-mode product rule written out once in closed
+   * form (SnavelyJacobianByHand); the default. */
+  CSE_JACOBIAN_CLOSED_FORM = 0,
+  /* Forward-mode dual numbers Jet<double, 12> seeded per parameter, as
+   * AutoDiffCostFunction / AutoDifferentiate (autodiff.h:314-381,
+   * autodiff_cost_function_cuda.h:55-71). */
+  CSE_JACOBIAN_JET = 1
+} cse_jacobian_form;
 
 typedef struct cse_evaluator cse_evaluator;
 

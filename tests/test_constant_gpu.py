@@ -256,3 +256,19 @@ def test_problem_13682_one_held_camera(gpu):
                   "problem-13682 held camera, no gradient", report=rep_ng)
     print("problem-13682 one-held-camera parity:", rep)
     print("problem-13682 one-held-camera parity, residual+Jacobian kernel:", rep_ng)
+
+
+def test_held_cameras_jet_form_take_the_table_path(gpu):
+    """jacobian_form = CSE_JACOBIAN_JET with held cameras: the Jet
+    instantiations exclude the held-camera kernels, so the group runs the
+    table kernel (with Jets), against the oracle."""
+    prog = held(counts=(12, 800, 3001), const=(0, 5), loss=ca.Loss.huber(1.0), seed=9)
+    ref = oracle_eval(prog)
+    ev = ca.Evaluator(prog, jacobian_form="jet")
+    try:
+        got = ev.evaluate()
+        info = ev.info()
+    finally:
+        ev.close()
+    assert info.num_affine_groups == 0
+    assert_parity(got, ref, "held cameras, Jet form")

@@ -109,8 +109,13 @@ def test_multi_device_shard_local_state_and_registered_buffers(gpu):
     finally:
         for a in (state, bufs[0], bufs[2]):
             ca.host_unregister(a)
-    with pytest.raises(RuntimeError, match="not registered"):
+    with pytest.raises(ValueError, match="not an array registered"):
         ca.host_unregister(state)
+    from ceres_amd import _cse
+    assert _cse.lib().cse_host_unregister(state.ctypes.data) < 0  # the library's own registry
+    assert "not registered" in _cse.lib().cse_last_error().decode()
+    with pytest.raises(TypeError):
+        ca.host_register(list(range(8)))  # only an ndarray, registered in place
     assert plain[1] == pinned[1] == again[1]
     assert all(np.array_equal(x, y) for x, y in zip(plain[2:], pinned[2:]))
     assert_parity(plain, ref, "shard-local multi")

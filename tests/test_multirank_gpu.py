@@ -118,3 +118,103 @@ def test_sharded_libcse_matches_unsharded_oracle(gpu, fmt, side_stream):
     results = dict(q.get(timeout=10) for _ in range(world))
     assert all(v == "ok" for v in results.values()), results
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _rccl_worker(port, backend, fmt, counts, q):
+    """One rank of a `backend` process group (world size 1) with the exchange
+    forced on: every collective of ShardedEvaluator runs, and with one rank
+    each all-reduce is the identity, so the outputs must equal a plain
+    evaluation of the same shard bit for bit."""
+    import sys
+    for p in (os.path.join(REPO, "ceres-solver-cuda_amd"), os.path.join(REPO, "oracle"),
+              os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import ceres_amd as ca
+    from ceres_amd import bal, distributed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        C, P, Obs = counts
+        cams, pts, ci, pi, obs = bal.synthetic(C, P, Obs, seed=41)
+        loss = ca.Loss.huber(1.0)
+        stream = torch.cuda.Stream()  # a non-default stream: ordering is exercised
+        se = distributed.ShardedEvaluator(cams, pts, ci, pi, obs, 0, 1, device=0, loss=loss,
+                                          format=fmt, gradient=True, stream=stream,
+                                          exchange=True)
+        assert se.exchange and se._host_reduce == (backend == "gloo")
+        out = {}
+        # overlapped cost all-reduces (async_op=True, one cost slot each), the
+        # camera rows in order, then wait_exchange on the evaluator's stream
+        costs = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(3)]
+        for c in costs:
+            se.evaluate(cost=c, overlap=True)
+        se.wait_exchange()
+        assert se.wait() == 0
+        torch.cuda.synchronize()
+        out["overlap_costs"] = [float(c.item()) for c in costs]
+        # ordered (overlap=False), the Jacobian at the same point too
+        se.evaluate(overlap=False)
+        se.evaluate(overlap=False, new_evaluation_point=False)
+        assert se.wait() == 0
+        torch.cuda.synchronize()
+        out["cost"] = float(se.cost.item())
+        out["r"] = se.residuals.cpu().numpy()
+        out["j"] = se.jacobian.cpu().numpy()
+        out["g"] = se.gradient.cpu().numpy()
+        se.close()
+        # the same shard through a plain evaluator (no collective at all)
+        ev = ca.Evaluator(se.program, device=0)
+        ok, c, r, g, j = ev.evaluate()
+        ev.close()
+        assert ok
+        assert all(x == c for x in out["overlap_costs"]), (out["overlap_costs"], c)
+        assert out["cost"] == c
+        assert np.array_equal(out["r"], r) and np.array_equal(out["j"], j)
+        assert np.array_equal(out["g"], g)
+        np.save(os.path.join(os.environ.get("TMPDIR", "/tmp"), f"rccl1_{backend}_{fmt}_{port}.npy"),
+                np.concatenate([[c], g[se._cam_rows[0]:se._cam_rows[1]]]))
+        q.put(("ok", backend))
+    except Exception as e:
+        import traceback
+        q.put((repr(e) + traceback.format_exc(), backend))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fmt", ["block_sparse", "compressed_row"])
+def test_rccl_exchange_world_size_one(gpu, fmt):
+    """The RCCL branch of ShardedEvaluator (distributed.py: device-tensor
+    all_reduce, async_op=True with wait_exchange, the camera-row reduce on
+    the evaluator's stream) executed once on the test box's GPU under an
+    `nccl` process group of one rank, and the same under gloo; both must
+    leave the plain evaluation's outputs unchanged."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    counts = (16, 2500, 12001)
+    got = {}
+    for backend in ("nccl", "gloo"):
+        q = ctx.Queue()
+        port = _free_port()
+        p = ctx.Process(target=_rccl_worker, args=(port, backend, fmt, counts, q))
+        p.start()
+        p.join(100)
+        if p.is_alive():
+            p.kill()
+            pytest.fail(f"{backend} rank hung")
+        msg, b = q.get(timeout=10)
+        assert msg == "ok", msg
+        assert p.exitcode == 0
+        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"rccl1_{backend}_{fmt}_{port}.npy")
+        got[backend] = np.load(path)
+        os.remove(path)
+    # RCCL and gloo exchanges give the same cost and camera rows
+    assert np.array_equal(got["nccl"], got["gloo"])

@@ -347,6 +347,52 @@ def test_device_entry_point_with_torch_buffers(gpu):
     ev.close()
 
 
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_jet_jacobian_form(gpu, fmt, mode):
+    """cse_options.jacobian_form = CSE_JACOBIAN_JET: the Snavely functor's
+    Jacobian by forward-mode Jet<double, 12> (AutoDifferentiate,
+    autodiff.h:314-381) on the same affine kernels, every gradient mode
+    (3 runs as the post-pass 1), against the oracle; the closed-form
+    default agrees with it to the parity bounds but not bit for bit (so the
+    option really selects another instantiation)."""
+    prog = small_bal(loss=ca.Loss.huber(1.0), fmt=fmt)
+    ref = oracle_eval(prog)
+    ev = ca.Evaluator(prog, jacobian_form="jet", gradient_mode=mode)
+    try:
+        got = ev.evaluate()
+        info = ev.info()
+        ng = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+        again = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    finally:
+        ev.close()
+    assert info.num_affine_groups == 1
+    assert info.num_fused_gradient_groups == (1 if mode == 0 else 0)
+    assert_parity(got, ref, ("jet", fmt, mode))
+    assert_parity(drop_gradient(ng), drop_gradient(ref), ("jet, no gradient", fmt))
+    assert np.array_equal(ng[4], again[4]) and ng[1] == again[1]
+    closed, _ = gpu_eval(prog, residuals=True, gradient=False, jacobian=True)
+    assert not np.array_equal(closed[4], ng[4])
+    assert is_approx(closed[4], ng[4])
+    with pytest.raises(ValueError):
+        ca.Evaluator(prog, jacobian_form="numeric")
+
+
+def test_jet_jacobian_form_table_path(gpu):
+    """Shapes the Jet instantiations do not cover run the table kernel with
+    Jets: forced general layout, and held cameras (test_constant_gpu)."""
+    prog = small_bal(loss=ca.Loss.cauchy(2.0))
+    ref = oracle_eval(prog)
+    ev = ca.Evaluator(prog, jacobian_form="jet", force_general_layout=True)
+    try:
+        got = ev.evaluate()
+        info = ev.info()
+    finally:
+        ev.close()
+    assert info.num_affine_groups == 0
+    assert_parity(got, ref, "jet table")
+
+
 @pytest.mark.slow
 def test_problem_13682_full_size(gpu):
     # BASELINE.json configs[3]: problem-13682 shape, Huber, BSM: the full
@@ -372,10 +418,23 @@ def test_problem_13682_full_size(gpu):
     ref = oracle_eval(prog, threads=16, residuals=True, gradient=True, jacobian=True)
     rep, rep_ng = {}, {}
     assert_parity(got, ref, "problem-13682", report=rep)
+    del got
     assert_parity(drop_gradient(got_ng), drop_gradient(ref), "problem-13682 no gradient",
                   report=rep_ng)
     print("problem-13682 BSM Huber parity:", rep)
     print("problem-13682 BSM Huber parity, residual+Jacobian kernel:", rep_ng)
+    del got_ng
+    # The Jet<double, 12> instantiation of the same kernel (bench.py
+    # secondary.jet; cse_options.jacobian_form = CSE_JACOBIAN_JET).
+    ev = ca.Evaluator(prog, jacobian_form="jet")
+    try:
+        got_jet = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    finally:
+        ev.close()
+    rep_jet = {}
+    assert_parity(drop_gradient(got_jet), drop_gradient(ref), "problem-13682 Jet form",
+                  report=rep_jet)
+    print("problem-13682 BSM Huber parity, Jet<12> residual+Jacobian kernel:", rep_jet)
 
 
 def test_gradient_post_pass_deterministic_and_agrees_with_atomics(gpu):
