@@ -331,12 +331,14 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
   cse::LaunchPipelinedSnavelyProbe<L, kStoreWaves, kOpt>(a, s);
 }
 
-// Tuning build: four-wave workgroups storing their four chunks' outputs as
-// long runs (tools/tuning/quad_kernel.hpp).  Variants 90, 91.
-template <class K, int L, int kSched>
+// Tuning build: kW-wave workgroups storing their kW chunks' outputs as long
+// runs (tools/tuning/quad_kernel.hpp).  Variants 90-97.
+template <class K, int L, int kW, int kSched, int kPad = 0>
 void LaunchQuad(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  hipLaunchKernelGGL((cse::EvaluateAffineQuad<K, L, kSched>), dim3((unsigned)num_wg),
-                     dim3(cse::kBlockThreads), 0, s, a);
+  (void)num_wg;
+  const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+  hipLaunchKernelGGL((cse::EvaluateAffineQuad<K, L, kW, kSched, kPad>), dim3((unsigned)((chunks + kW - 1) / kW)),
+                     dim3(kW * cse::kWave), 0, s, a);
 }
 
 // Tuning build: the BlockSparseMatrix Jacobian evaluation of the Snavely
@@ -564,8 +566,14 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 84: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 4>>;
     case 85: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 5>>;
     // four-wave workgroups, long store runs (quad_kernel.hpp)
-    case 90: return &LaunchQuad<K, L, 0>;
-    case 91: return &LaunchQuad<K, L, 1>;
+    case 90: return &LaunchQuad<K, L, 4, 0>;     // 4 waves, 13 KiB each; 12 waves per CU
+    case 91: return &LaunchQuad<K, L, 4, 1>;     // 4 waves, F in thirds + E and R
+    case 92: return &LaunchQuad<K, L, 2, 0>;     // 2 waves; 12 waves per CU
+    case 93: return &LaunchQuad<K, L, 3, 0>;     // 3 waves; 12 waves per CU
+    case 94: return &LaunchQuad<K, L, 4, 0, 28>; // 4 waves; 8 waves per CU
+    case 95: return &LaunchQuad<K, L, 8, 0>;     // 8 waves; 8 waves per CU
+    case 96: return &LaunchQuad<K, L, 5, 0>;     // 5 waves; 10 waves per CU
+    case 97: return &LaunchQuad<K, L, 6, 0>;     // 6 waves; 12 waves per CU
     default: return nullptr;
   }
 }
@@ -1616,7 +1624,9 @@ const char* cse_last_error(void) { return g_last_error.c_str(); }
 int cse_abi_version(void) { return CSE_ABI_VERSION; }
 
 const char* cse_build_info(void) {
-  return "cse abi=1 target=gfx950 built " __DATE__ " " __TIME__;
+#define CSE_STR2_(x) #x
+#define CSE_STR_(x) CSE_STR2_(x)
+  return "cse abi=" CSE_STR_(CSE_ABI_VERSION) " target=gfx950 built " __DATE__ " " __TIME__;
 }
 
 int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evaluator** out) {

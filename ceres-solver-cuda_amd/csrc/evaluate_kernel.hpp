@@ -1618,7 +1618,7 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
 // The sorted slot-1 ids streamed non-temporally (1) or with the default
 // policy (0), like the functor data.
 #ifndef CSE_CAMGRAD_NT_IDS
-#define CSE_CAMGRAD_NT_IDS 0
+#define CSE_CAMGRAD_NT_IDS 1
 #endif
 // CSE_CAMGRAD_WAVES: a lower bound on its waves per SIMD (A/B builds; 1 = the
 // compiler's choice, 158 VGPRs = 3 with the by-hand functor).
