@@ -1615,6 +1615,14 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
   }
 }
 
+// CameraGradientKernel's camera rows for the Snavely camera: by the reverse
+// sweep SnavelyCameraRowVjp (1) or by forming J0 by hand and contracting it
+// with the corrected residuals (0).
+#ifndef CSE_CAMGRAD_VJP
+#define CSE_CAMGRAD_VJP 0
+#endif
+template <class K>
+constexpr bool kCamGradVjp = std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0 && CSE_CAMGRAD_VJP != 0;
 // The sorted slot-1 ids streamed non-temporally (1) or with the default
 // policy (0), like the functor data.
 #ifndef CSE_CAMGRAD_NT_IDS
@@ -1682,6 +1690,25 @@ CameraGradientKernel(const CamGradArgs g) {
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
+      if constexpr (kCamGradVjp<K>) {
+        // the camera row by a reverse sweep (SnavelyCameraRowVjp)
+        double r[NR], gv[S0];
+        const bool robust = (kLoss != kLossTrivial || g.loss.scaled) && g.apply_loss;
+        SnavelyCameraRowVjp(
+            d[u], x0, x1[u],
+            [&](double sq) {
+              if (!robust) return 1.0;
+              double rho[3];
+              EvaluateLoss<kLoss>(g.loss, sq, rho);
+              return rho[1];
+            },
+            r, gv);
+        if (live[u]) {
+#pragma unroll
+          for (int c = 0; c < S0; ++c) acc[c] += gv[c];
+        }
+        continue;
+      }
       double r[NR], J0[NR * S0], J1[NR * S1p];
       EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
 #pragma unroll

@@ -27,8 +27,8 @@
 #   variants ROUNDS MODE V,V,.. [FLAGS]
 #                         tools/ab_bench.py over the tuning build's variants
 #   configs [LIST]        tools/run_configs.sh (LIST: newline-separated args)
-#   pmc [BENCH_ARGS]      per-kernel PMC passes + HBM traffic JSON of the
-#                         headline kernel (tools/gpu_pmc_kernels.sh)
+#   pmc [BENCH_ARGS]      per-kernel PMC passes (tools/gpu_pmc_kernels.sh); with
+#                         no BENCH_ARGS (the headline) also its HBM traffic JSON
 #   cmd ...               any other command, under a 600 s limit
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -96,8 +96,10 @@ for step in "$@"; do
       BENCH_ARGS=${args:-"--no-cpu-baseline --no-secondary --steps 5 --warmup 1"} \
         bash tools/gpu_pmc_kernels.sh $TAG/pmc_$n > /dev/null || exit 1
       cat $OUT/pmc_$n/pmc_by_kernel.txt | head -40
-      python3 tools/pmc_traffic_json.py $OUT/pmc_$n/pmc1 $OUT/pmc_$n/pmc2 EvaluateAffineChunksTwoRoundW1 \
-        $OUT/pmc_problem-13682-4456117_huber_block_sparse.json "tools/gpu_run.sh pmc, $TAG" || exit 1 ;;
+      if [ -z "$args" ]; then  # the headline: its HBM traffic JSON for bench.py
+        python3 tools/pmc_traffic_json.py $OUT/pmc_$n/pmc1 $OUT/pmc_$n/pmc2 EvaluateAffineChunksTwoRoundW1 \
+          $OUT/pmc_problem-13682-4456117_huber_block_sparse.json "tools/gpu_run.sh pmc, $TAG" || exit 1
+      fi ;;
     cmd)
       timeout -k 10 600 bash -c "$args" > $OUT/cmd_$n.txt 2>&1 || { echo "cmd rc=$?"; tail -20 $OUT/cmd_$n.txt; exit 1; }
       tail -30 $OUT/cmd_$n.txt ;;
