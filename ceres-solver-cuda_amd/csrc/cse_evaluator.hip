@@ -565,6 +565,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 83: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 3>>;
     case 84: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 4>>;
     case 85: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 5>>;
+    // the shipped kernel with the slot-0 ids of full chunks through the scalar cache
+    case 86: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 0, 0, false, false, 0, 0, 0, false, false, true>>;
     // four-wave workgroups, long store runs (quad_kernel.hpp)
     case 90: return &LaunchQuad<K, L, 4, 0>;     // 4 waves, 13 KiB each; 12 waves per CU
     case 91: return &LaunchQuad<K, L, 4, 1>;     // 4 waves, F in thirds + E and R

@@ -643,7 +643,7 @@ template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinL
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
           int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
           int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0, bool kConst0_ = false,
-          bool kXcdMap_ = false>
+          bool kXcdMap_ = false, bool kScalarIds_ = false>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -664,6 +664,10 @@ struct Tune {
   // Workgroups dispatched round-robin over the 8 XCDs get contiguous chunk
   // ranges per XCD (workgroup b -> XCD b % 8, remapped to a bijection).
   static constexpr bool kXcdMap = kXcdMap_;
+  // Full chunks read their 64 slot-0 ids through the scalar cache (s_load,
+  // then v_writelane), so the camera gather's addresses do not wait on a
+  // vector load queued behind other waves' stores (tuning build).
+  static constexpr bool kScalarIds = kScalarIds_;
 };
 
 // The logical workgroup of dispatch index b when each of the 8 XCDs is to
@@ -804,6 +808,32 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (Tr::NB == 2) {
       const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
       id = make_int2((int)b, (int)(b >> 32));
+#ifdef CSE_TUNING
+      if constexpr (T::kScalarIds && kWPB == 1) {
+        if (nw == kWave) {  // uniform branch: the whole chunk exists
+          typedef int cse_s16 __attribute__((ext_vector_type(16)));
+          const uint64_t addr = reinterpret_cast<uint64_t>(a.ids + 2 * i0);
+          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
+          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
+          const uint64_t base = ((uint64_t)hi << 32) | lo;
+          int cx = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // 4 x 16 dwords = 32 (camera, point) pairs per half
+            cse_s16 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(v[k]) : "s"(base), "i"(256 * h + 64 * k));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(cx) : "s"(v[k][2 * j]), "i"(32 * h + 8 * k + j));
+          }
+          id.x = cx;
+        }
+      }
+#endif
     } else {
       id = LoadIds<K>(a, i);
     }
