@@ -690,7 +690,7 @@ def main():
                 "kernel_ms_avg": kernel_ms,
                 "kernel_ms_avg_max_rank": kernel_ms_max,
                 "kernel": f"cse::EvaluateAffineChunks"
-                          f"{'FusedPointsW1' if args.gradient else ('TwoRoundW1' if args.format == 'block_sparse' else 'TwoRoundCrsW1')}"
+                          f"{'FusedPointsW1' if args.gradient else (('GroupStore' if not quat and not args.held_cameras else 'TwoRoundW1') if args.format == 'block_sparse' else 'TwoRoundCrsW1')}"
                           f"<{'SnavelyQuaternionTangentKind' if quat else 'SnavelyKind'}, {args.loss}, {args.format}> (+ repack"
                           f"{', CameraGradientKernel and the gradient tail' if args.gradient else ''})",
                 "per": "GPU (bytes of all ranks / N over the slowest rank's kernel time)",

@@ -24,13 +24,13 @@
 #include <vector>
 
 #include "../../include/cse.h"
+#include "group_store_kernel.hpp"
 #include "jet_kernels.h"
 #include "multi_device.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
 #include "../../tools/tuning/persistent_launch.h"  // tuning build only
 #include "../../tools/tuning/pipeline_launch.h"    // tuning build only
-#include "../../tools/tuning/quad_kernel.hpp"      // tuning build only
 #endif
 
 namespace {
@@ -296,8 +296,26 @@ void LaunchChunks(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 #ifndef CSE_TWOROUND_W1
 #define CSE_TWOROUND_W1 1
 #endif
+// The Snavely camera's BSM residual+Jacobian evaluation, when its outputs sit
+// on 64-byte sectors: four-wave workgroups storing long runs
+// (group_store_kernel.hpp; CSE_GROUP_STORE 0 keeps the one-wave kernel).
+#ifndef CSE_GROUP_STORE
+#define CSE_GROUP_STORE 1
+#endif
+template <class K, class T>
+constexpr bool kGroupStore = CSE_GROUP_STORE != 0 && std::is_same<K, cse::SnavelyKind>::value &&
+                             std::is_same<T, cse::ShippedTune>::value && CSE_BY_HAND != 0;
+
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRound(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  if constexpr (kGroupStore<K, T> && Co == 2) {
+    if (cse::GroupStoreEligible(a)) {
+      const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+      hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, 4, 0, 0>), dim3((unsigned)((chunks + 3) / 4)),
+                         dim3(4 * cse::kWave), 0, s, a);
+      return;
+    }
+  }
   if constexpr (CSE_TWOROUND_W1 != 0) {
     const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundW1<K, L, Co, T>), dim3((unsigned)chunks),
@@ -331,13 +349,68 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
   cse::LaunchPipelinedSnavelyProbe<L, kStoreWaves, kOpt>(a, s);
 }
 
+template <class K, int L>
+void LaunchW1Only(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  (void)num_wg;
+  const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundW1<K, L, 2, cse::ShippedTune>), dim3((unsigned)chunks),
+                     dim3(cse::kWave), 0, s, a);
+}
+
+// Tuning build: the shipped BSM kernel with per-wave phase stamps (Tune::
+// kProbe); every 20th launch prints the phase durations' distribution.
+template <class K, int L>
+void LaunchTwoRoundProbe(const cse::GroupArgs& a0, int64_t num_wg, hipStream_t s) {
+  using T = cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 0, 0, false, false, 0, 0, 0,
+                      false, false, false, true>;
+  static unsigned long long* buf = nullptr;
+  static int64_t cap = 0;
+  static int launches = 0;
+  const int64_t chunks = (a0.n + cse::kWave - 1) / cse::kWave;
+  if (chunks > cap) {
+    if (buf) (void)hipFree(buf);
+    (void)hipMalloc(&buf, (size_t)chunks * 8 * sizeof(unsigned long long));
+    cap = chunks;
+  }
+  (void)hipMemsetAsync(buf, 0, (size_t)chunks * 8 * sizeof(unsigned long long), s);
+  cse::GroupArgs a = a0;
+  a.probe = buf;
+  LaunchTwoRound<K, L, 2, T>(a, num_wg, s);
+  if (++launches % 20 != 0) return;
+  (void)hipStreamSynchronize(s);
+  std::vector<unsigned long long> h((size_t)chunks * 8);
+  (void)hipMemcpy(h.data(), buf, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  std::vector<double> ph[4];
+  unsigned long long rt_min = ~0ull, rt_max = 0;
+  for (int64_t c = 0; c < chunks; ++c) {
+    const unsigned long long* o = &h[(size_t)c * 8];
+    if (o[5] != 1) continue;
+    for (int k = 0; k < 4; ++k) ph[k].push_back((double)o[k]);
+    rt_min = std::min(rt_min, o[4]);
+    rt_max = std::max(rt_max, o[4]);
+  }
+  const char* names[4] = {"ids", "gather", "compute", "store-issue"};
+  fprintf(stderr, "# probe: %zu waves, starts spread over %.1f us;", ph[0].size(),
+          (double)(rt_max - rt_min) * 0.01);
+  for (int k = 0; k < 4; ++k) {
+    auto& v = ph[k];
+    if (v.empty()) continue;
+    std::sort(v.begin(), v.end());
+    double sum = 0;
+    for (double x : v) sum += x;
+    fprintf(stderr, " %s mean %.0f p10 %.0f p50 %.0f p90 %.0f cyc;", names[k], sum / v.size(),
+            v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10]);
+  }
+  fprintf(stderr, "\n");
+}
+
 // Tuning build: kW-wave workgroups storing their kW chunks' outputs as long
-// runs (tools/tuning/quad_kernel.hpp).  Variants 90-97.
+// runs (group_store_kernel.hpp; the product launches kW = 4).  Variants 90-98.
 template <class K, int L, int kW, int kSched, int kPad = 0>
 void LaunchQuad(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
   const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-  hipLaunchKernelGGL((cse::EvaluateAffineQuad<K, L, kW, kSched, kPad>), dim3((unsigned)((chunks + kW - 1) / kW)),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad>), dim3((unsigned)((chunks + kW - 1) / kW)),
                      dim3(kW * cse::kWave), 0, s, a);
 }
 
@@ -567,7 +640,9 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 85: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 5>>;
     // the shipped kernel with the slot-0 ids of full chunks through the scalar cache
     case 86: return &LaunchTwoRound<K, L, 2, cse::Tune<0, true, true, 0, 64, CSE_STORE_ORDER, false, false, 0, 0, false, false, 0, 0, 0, false, false, true>>;
-    // four-wave workgroups, long store runs (quad_kernel.hpp)
+    // the shipped kernel with per-wave phase stamps
+    case 87: return &LaunchTwoRoundProbe<K, L>;
+    // kW-wave workgroups, long store runs (group_store_kernel.hpp)
     case 90: return &LaunchQuad<K, L, 4, 0>;     // 4 waves, 13 KiB each; 12 waves per CU
     case 91: return &LaunchQuad<K, L, 4, 1>;     // 4 waves, F in thirds + E and R
     case 92: return &LaunchQuad<K, L, 2, 0>;     // 2 waves; 12 waves per CU
@@ -576,6 +651,11 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 95: return &LaunchQuad<K, L, 8, 0>;     // 8 waves; 8 waves per CU
     case 96: return &LaunchQuad<K, L, 5, 0>;     // 5 waves; 10 waves per CU
     case 97: return &LaunchQuad<K, L, 6, 0>;     // 6 waves; 12 waves per CU
+    // the Jet<12> functor (SnavelyJetKind): the four-wave long-run kernel and the shipped one
+    case 98: return &LaunchQuad<cse::SnavelyJetKind, L, 4, 0>;
+    case 99: return &LaunchTwoRound<cse::SnavelyJetKind, L, 2>;
+    // the one-wave-workgroup kernel the group-store kernel replaced (round 4's headline)
+    case 80: return &LaunchW1Only<K, L>;
     default: return nullptr;
   }
 }

@@ -643,7 +643,7 @@ template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinL
           int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
           int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
           int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0, bool kConst0_ = false,
-          bool kXcdMap_ = false, bool kScalarIds_ = false>
+          bool kXcdMap_ = false, bool kScalarIds_ = false, bool kProbe_ = false>
 struct Tune {
   static constexpr int kPrio = kPrio_;
   static constexpr bool kLdsE = kLdsE_;
@@ -668,6 +668,9 @@ struct Tune {
   // then v_writelane), so the camera gather's addresses do not wait on a
   // vector load queued behind other waves' stores (tuning build).
   static constexpr bool kScalarIds = kScalarIds_;
+  // Per-wave phase stamps (s_memtime) into a.probe[chunk][8]: ids arrived,
+  // gather arrived, outputs ready, stores issued (tuning build).
+  static constexpr bool kProbe = kProbe_;
 };
 
 // The logical workgroup of dispatch index b when each of the 8 XCDs is to
@@ -802,12 +805,24 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   }
 
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(2);
+  unsigned long long pt[5] = {0, 0, 0, 0, 0};  // T::kProbe stamps
+  auto stamp = [&](int k) {
+    if constexpr (T::kProbe) pt[k] = __builtin_amdgcn_s_memtime();
+  };
+  if constexpr (T::kProbe) {
+    stamp(0);
+    pt[4] = __builtin_amdgcn_s_memrealtime();
+  }
   AffineInputs<K> in;
   if constexpr (kCoop == 2) {
     int2 id;
     if constexpr (Tr::NB == 2) {
       const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
       id = make_int2((int)b, (int)(b >> 32));
+      if constexpr (T::kProbe) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(1);
+      }
 #ifdef CSE_TUNING
       if constexpr (T::kScalarIds && kWPB == 1) {
         if (nw == kWave) {  // uniform branch: the whole chunk exists
@@ -860,6 +875,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     GatherCoop<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
   }
   if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(0);
+  stamp(2);
   // The chunk bounds' first use, after the gather: their scalar loads were
   // issued before it and have long arrived (without the pin the compiler
   // compares them right away and waits for them before the gather starts).
@@ -1385,6 +1401,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(flast), "v"(elast));
 
+  stamp(3);
   // ---- every store of the wave, back to back ----
   auto store_f = [&]() {
 #ifdef CSE_TUNING
@@ -1462,6 +1479,18 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if (lane == 0) {
     StoreB64(v_partial, v_wsum);
     if (failed) StoreB32(status_dst, 1);
+  }
+  if constexpr (T::kProbe) {
+    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && a.probe) {
+      unsigned long long* o = a.probe + 8 * c;
+      o[0] = pt[1] - pt[0];  // the ids load
+      o[1] = pt[2] - pt[1];  // the camera gather, observations and points
+      o[2] = pt[3] - pt[2];  // functor, loss, staging, addresses
+      o[3] = t4 - pt[3];     // issuing the store tail
+      o[4] = pt[4];          // s_memrealtime at the start (100 MHz)
+      o[5] = 1;
+    }
   }
   KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
   KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);

@@ -1,27 +1,34 @@
-// quad_kernel.hpp -- tuning build only (-DCSE_TUNING): the BlockSparseMatrix
-// residual+Jacobian kernel with kW-wave workgroups over kW consecutive
-// 64-block chunks whose F cells, E cells and residuals are staged together in
-// LDS and then written as long contiguous runs, each wave storing one to
-// three runs of the workgroup's output instead of its own chunk's three
-// segments.
+// group_store_kernel.hpp -- the BlockSparseMatrix residual+Jacobian kernel
+// of the Snavely camera with kW-wave workgroups over kW consecutive 64-block
+// chunks (shipped: kW = 4, EvaluateAffineChunksGroupStore).  Each wave
+// evaluates its chunk as EvaluateAffineChunksTwoRoundW1 does (LDS-DMA camera
+// gather, the closed-form functor, loss and Corrector, cost partial in the
+// same slot); then the workgroup's F cells, E cells and residuals are staged
+// together in LDS, in output order, and written as long contiguous runs:
+// the workgroup's four chunks own one 36 KiB F run, one 12 KiB E run and one
+// 4 KiB residual run (block_jacobian_writer.cc:75-149: all E cells, then all
+// F cells, in block order), 52 KiB of LDS (3 workgroups, 12 waves per CU),
+// and the image [F | E | R] is cut into 13 KiB per wave (kSched 0): wave 0
+// stores F[0, 13 KiB), wave 1 F[13, 26), wave 2 F[26, 36) and E[0, 3), wave
+// 3 E[3, 12) and the residuals -- one or two runs a wave instead of three
+// short segments (9, 3 and 1 KiB) per wave.
 //
-// The hypothesis it tests: the shipped
-// kernel (EvaluateAffineChunksTwoRoundW1) reaches 0.61-0.66 of 8 TB/s while a
-// pure 16-B write stream of its bytes reaches 0.72-0.74, and the gap is the
-// interleaving of every resident wave's three short output streams (9 KiB of
-// F, 3 KiB of E, 1 KiB of residuals).  Here the workgroup's kW chunks own
-// one contiguous 9 kW KiB F run, one 3 kW KiB E run and one kW KiB residual
-// run (block_jacobian_writer.cc:75-149: all E cells, then all F cells, in
-// block order), staged in 13 kW KiB of LDS; the image [F | E | R] is cut
-// into 13 KiB per wave (kSched 0), or (kSched 1, kW = 4) waves 0-2 take F in
-// thirds and wave 3 all of E and R (the schedule VERDICT r4 named).
-// kPadKiB: extra LDS per workgroup (an occupancy limit).
-// Outputs are bit-identical to the shipped kernel's (same functor, loss,
-// cost partial per wave in the same slot).
-#ifndef CSE_QUAD_KERNEL_HPP_
-#define CSE_QUAD_KERNEL_HPP_
+// Measured (same-process interleaved A/Bs against the
+// one-wave-workgroup kernel, bit-identical outputs): -1.6 %, -1.4 %, -2.3 %
+// on three boxes (profiles/round5/r5a, r5b, r5c).  Other shapes of the
+// tuning build (kW = 2, 3, 5, 6, 8; 8 waves per CU; waves 0-2 taking F in
+// thirds and wave 3 E and R, kSched 1) were slower.
+//
+// Used when the group's residual, E and F bases are 64-byte aligned (then
+// every workgroup's runs are: 9216, 3072 and 1024 bytes per chunk) and both
+// outputs are requested; otherwise the one-wave kernel, whose sector-window
+// tail handles any alignment.  The last, partial workgroup stores each
+// chunk through the slow tail.  Gradient atomics (gradient_mode 2) as the
+// one-wave kernel.
+#ifndef CSE_GROUP_STORE_KERNEL_HPP_
+#define CSE_GROUP_STORE_KERNEL_HPP_
 
-#include "../../ceres-solver-cuda_amd/csrc/evaluate_kernel.hpp"
+#include "evaluate_kernel.hpp"
 
 namespace cse {
 
@@ -104,7 +111,7 @@ constexpr int kQuadWavesPerEu = ((160 / (13 * kW + kPadKiB)) * kW + 3) / 4;
 
 template <class K, int kLoss, int kW, int kSched, int kPadKiB>
 __global__ __launch_bounds__(kW * kWave) __attribute__((amdgpu_waves_per_eu(kQuadWavesPerEu<kW, kPadKiB>))) void
-EvaluateAffineQuad(const GroupArgs a) {
+EvaluateAffineChunksGroupStore(const GroupArgs a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   static_assert(NR == 2 && S0 == 9 && S1 == 3, "Snavely-shaped kinds");
@@ -136,6 +143,10 @@ EvaluateAffineQuad(const GroupArgs a) {
     if (ok && a.check_finite)
       ok = !(AnyNonFinite<NR>(r) || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1));
     cost = LossAndCorrect<K, kLoss, true>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
+    if (a.gradient != nullptr && active) {  // gradient_mode 2: FP64 atomics, as the reference
+      AddGradientSlot<NR, S0>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0, S0, r, J0);
+      AddGradientSlot<NR, S1p>(a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1, S1, r, J1);
+    }
   }
   const double wsum = WaveSumLane0(active ? cost : 0.0);
   const bool failed = __ballot(active && !ok) != 0;
@@ -173,6 +184,16 @@ EvaluateAffineQuad(const GroupArgs a) {
   }
 }
 
+// May the group take EvaluateAffineChunksGroupStore?  Both outputs, and the
+// residual, E-cell and F-cell bases on 64-byte sectors.
+inline bool GroupStoreEligible(const GroupArgs& a) {
+  if (!a.residuals || !a.jacobian) return false;
+  const uintptr_t m = reinterpret_cast<uintptr_t>(a.residuals + a.res_base) |
+                      reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[0][0]) |
+                      reinterpret_cast<uintptr_t>(a.jacobian + a.jac_base[1][0]);
+  return (m & 63) == 0 && a.jac_stride[0] == 18 && a.jac_stride[1] == 6;
+}
+
 }  // namespace cse
 
-#endif  // CSE_QUAD_KERNEL_HPP_
+#endif  // CSE_GROUP_STORE_KERNEL_HPP_

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--held-tail", type=int, default=0,
                     help="append one held camera observed by the last K blocks only (the "
                          "held-camera kernels on an otherwise aligned layout)")
+    ap.add_argument("--jacobian-form", default="closed", choices=["closed", "jet"],
+                    help="cse_options.jacobian_form of the evaluators (product kernels)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="time rank 0's shard of an N-way point-bucket cut instead")
     args = ap.parse_args()
@@ -92,7 +94,8 @@ def main():
                 os.environ["CSE_TUNE_CAMSTRIDE"] = cs
             else:
                 os.environ.pop("CSE_TUNE_CAMSTRIDE", None)
-            ev = ca.Evaluator(prog, device=0, profile=True, stream=stream.cuda_stream)
+            ev = ca.Evaluator(prog, device=0, profile=True, stream=stream.cuda_stream,
+                              jacobian_form=args.jacobian_form)
             info = ev.info()
             bytes_ = {"jacobian": info.bytes_jacobian_eval, "residual": info.bytes_residual_eval,
                       "gradient": info.bytes_jacobian_eval + 8 * prog.num_effective_parameters,

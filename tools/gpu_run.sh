@@ -23,7 +23,7 @@
 #                         tools/ab_bench.py, interleaved processes: LIB is a
 #                         directory under ceres-solver-cuda_amd/lib (empty =
 #                         lib/libcse.so), FLAGS extra ab_bench flags with '='
-#                         between flag and value
+#                         between flag and value and ',' between flags
 #   variants ROUNDS MODE V,V,.. [FLAGS]
 #                         tools/ab_bench.py over the tuning build's variants
 #   configs [LIST]        tools/run_configs.sh (LIST: newline-separated args)
@@ -78,8 +78,9 @@ for step in "$@"; do
           IFS=: read name lib flags <<< "$v"
           lp=$L/libcse.so; [ -n "$lib" ] && lp=$L/$lib/libcse.so
           f=$OUT/ab_${n}_${name}_$r.txt
+          fl=${flags//=/ }
           timeout -k 10 300 python -u tools/ab_bench.py --lib $lp --variants 0 --rounds 2 --steps 20 \
-            --mode $mode ${flags//=/ } > $f 2>&1 || { echo "ab $v rc=$?"; tail -5 $f; exit 1; }
+            --mode $mode ${fl//,/ } > $f 2>&1 || { echo "ab $v rc=$?"; tail -5 $f; exit 1; }
           echo "$name r$r: $(summ $f)"
         done
       done ;;
@@ -97,7 +98,7 @@ for step in "$@"; do
         bash tools/gpu_pmc_kernels.sh $TAG/pmc_$n > /dev/null || exit 1
       cat $OUT/pmc_$n/pmc_by_kernel.txt | head -40
       if [ -z "$args" ]; then  # the headline: its HBM traffic JSON for bench.py
-        python3 tools/pmc_traffic_json.py $OUT/pmc_$n/pmc1 $OUT/pmc_$n/pmc2 EvaluateAffineChunksTwoRoundW1 \
+        python3 tools/pmc_traffic_json.py $OUT/pmc_$n/pmc1 $OUT/pmc_$n/pmc2 EvaluateAffineChunksGroupStore \
           $OUT/pmc_problem-13682-4456117_huber_block_sparse.json "tools/gpu_run.sh pmc, $TAG" || exit 1
       fi ;;
     cmd)
