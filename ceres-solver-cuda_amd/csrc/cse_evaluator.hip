@@ -30,6 +30,7 @@
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
 #include "../../tools/tuning/persistent_launch.h"  // tuning build only
+#include "../../tools/tuning/pgs_launch.h"         // tuning build only
 #include "../../tools/tuning/pipeline_launch.h"    // tuning build only
 #endif
 
@@ -349,6 +350,18 @@ void LaunchPipelinedProbe(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s
   cse::LaunchPipelinedSnavelyProbe<L, kStoreWaves, kOpt>(a, s);
 }
 
+// Tuning build: the persistent pipelined group-store kernel (variant 88;
+// tools/tuning/pgs_kernel.hpp), the group-store kernel where not eligible.
+template <class K, int L>
+void LaunchPgs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  static_assert(std::is_same<K, cse::SnavelyKind>::value, "Snavely only");
+  if (cse::GroupStoreEligible(a)) {
+    cse::LaunchGroupStorePipelinedSnavely<L>(a, s);
+    return;
+  }
+  LaunchTwoRound<K, L, 2>(a, num_wg, s);
+}
+
 template <class K, int L>
 void LaunchW1Only(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
@@ -656,6 +669,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 99: return &LaunchTwoRound<cse::SnavelyJetKind, L, 2>;
     // the one-wave-workgroup kernel the group-store kernel replaced (round 4's headline)
     case 80: return &LaunchW1Only<K, L>;
+    // the group-store kernel, persistent and software-pipelined
+    case 88: return &LaunchPgs<K, L>;
     default: return nullptr;
   }
 }
