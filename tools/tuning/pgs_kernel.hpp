@@ -32,7 +32,12 @@ typedef double pgs_v2d __attribute__((ext_vector_type(2)));
 
 // Byte offsets inside a wave's F region (9 KiB) of the landing areas: camera
 // rows [0, 5 KiB), observations, the points' two 12-byte pieces.
-constexpr uint32_t kPgsObsOff = 5 * 1024, kPgsPtOff0 = 6 * 1024, kPgsPtOff1 = 6 * 1024 + 768;
+// (x, y) by one 16-byte piece a lane, z by two 4-byte pieces: widths whose
+// lane-linear LDS layout is certain (16 and 4 bytes a lane).
+constexpr uint32_t kPgsObsOff = 5 * 1024, kPgsXyOff = 6 * 1024, kPgsZloOff = 7 * 1024,
+                   kPgsZhiOff = 7 * 1024 + 256,
+                   // the ids of the chunk after next: (camera, point), 4 bytes a lane each
+                   kPgsIdcOff = 7 * 1024 + 512, kPgsIdpOff = 7 * 1024 + 768;
 
 // The observation pair and the point of `lane` from the landing areas.
 __device__ __forceinline__ void PgsReadInputs(const double* fw, int lane, double* d, double* x1) {
@@ -40,12 +45,12 @@ __device__ __forceinline__ void PgsReadInputs(const double* fw, int lane, double
   const double2 ob = *reinterpret_cast<const double2*>(b + kPgsObsOff + 16 * lane);
   d[0] = ob.x;
   d[1] = ob.y;
-  const uint32_t* p0 = reinterpret_cast<const uint32_t*>(b + kPgsPtOff0 + 12 * lane);
-  const uint32_t* p1 = reinterpret_cast<const uint32_t*>(b + kPgsPtOff1 + 12 * lane);
-  const uint32_t w0 = p0[0], w1 = p0[1], w2 = p0[2], w3 = p1[0], w4 = p1[1], w5 = p1[2];
-  x1[0] = __builtin_bit_cast(double, ((uint64_t)w1 << 32) | w0);
-  x1[1] = __builtin_bit_cast(double, ((uint64_t)w3 << 32) | w2);
-  x1[2] = __builtin_bit_cast(double, ((uint64_t)w5 << 32) | w4);
+  const double2 xy = *reinterpret_cast<const double2*>(b + kPgsXyOff + 16 * lane);
+  const uint32_t zlo = *reinterpret_cast<const uint32_t*>(b + kPgsZloOff + 4 * lane);
+  const uint32_t zhi = *reinterpret_cast<const uint32_t*>(b + kPgsZhiOff + 4 * lane);
+  x1[0] = xy.x;
+  x1[1] = xy.y;
+  x1[2] = __builtin_bit_cast(double, ((uint64_t)zhi << 32) | zlo);
 }
 
 // 16-byte store at SGPR base + VGPR offset + kOff bytes, `sc1 nt`.
@@ -82,7 +87,7 @@ __device__ __forceinline__ void PgsStores(double* const bases[3], uint32_t voff,
 template <class K>
 __device__ __forceinline__ void PgsIssueGather(const GroupArgs& a, double* lds, int64_t c, long long id,
                                                int64_t cn, int lane, pgs_v2d* o, double* p,
-                                               long long* idn) {
+                                               long long* idn, uint32_t ids_lds) {
   using Tr = KindTraits<K>;
   constexpr int X0 = Tr::X0, X0p = (X0 + 1) & ~1, kPieces = X0p / 2;
   constexpr int kRow = PackedRowDoubles(X0);
@@ -106,18 +111,29 @@ __device__ __forceinline__ void PgsIssueGather(const GroupArgs& a, double* lds, 
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(po), "s"(mo)
                : "memory");
   const double* pt = a.state + a.state_base[1] + 3LL * pid;
-  const uint32_t mp0 = __builtin_amdgcn_readfirstlane(lbase + kPgsPtOff0);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx3 %0, off nt" ::"v"(pt), "s"(mp0)
+  const uint32_t mxy = __builtin_amdgcn_readfirstlane(lbase + kPgsXyOff);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(pt), "s"(mxy)
                : "memory");
-  const uint32_t mp1 = __builtin_amdgcn_readfirstlane(lbase + kPgsPtOff1);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx3 %0, off offset:12 nt" ::"v"(pt),
-               "s"(mp1)
+  const uint32_t mzl = __builtin_amdgcn_readfirstlane(lbase + kPgsZloOff);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off offset:16 nt" ::"v"(pt),
+               "s"(mzl)
+               : "memory");
+  const uint32_t mzh = __builtin_amdgcn_readfirstlane(lbase + kPgsZhiOff);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off offset:20 nt" ::"v"(pt),
+               "s"(mzh)
                : "memory");
   (void)o;
   (void)p;
-  if (cn >= 0) {
-    const long long* pi = reinterpret_cast<const long long*>(a.ids) + cn * kWave + lane;
-    asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(*idn) : "v"(pi) : "memory");
+  (void)idn;
+  if (cn >= 0) {  // into a second id slot (the current ids were read from the first)
+    const int32_t* pi = a.ids + 2 * (cn * kWave + lane);
+    const uint32_t mic = __builtin_amdgcn_readfirstlane(ids_lds + kPgsIdcOff);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(pi), "s"(mic)
+                 : "memory");
+    const uint32_t mip = __builtin_amdgcn_readfirstlane(ids_lds + kPgsIdpOff);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off offset:4 nt" ::"v"(pi),
+                 "s"(mip)
+                 : "memory");
   }
 }
 
@@ -137,6 +153,7 @@ EvaluateGroupStorePipelined(const GroupArgs a, int64_t nfull) {
   double* rw = img + (kQuadFk + kQuadEk) * 4 * 128 + w * (NR * kWave);
   const int64_t G = gridDim.x;
   const uint32_t voff = 16u * lane;
+  const uint32_t ids_lds = (uint32_t)reinterpret_cast<uintptr_t>(fw);
   int64_t q = blockIdx.x;
   long long idn = 0, idnn = 0;
   pgs_v2d o = {0.0, 0.0}, on = {0.0, 0.0};  // (unused: the inputs land in LDS)
@@ -148,8 +165,9 @@ EvaluateGroupStorePipelined(const GroupArgs a, int64_t nfull) {
     long long id0;
     const long long* pi = reinterpret_cast<const long long*>(a.ids) + (q * 4 + w) * kWave + lane;
     asm volatile("global_load_dwordx2 %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(id0) : "v"(pi) : "memory");
-    PgsIssueGather<K>(a, fw, q * 4 + w, id0, q + G < nfull ? (q + G) * 4 + w : -1, lane, &o, pt, &idn);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(idn) : : "memory");
+    PgsIssueGather<K>(a, fw, q * 4 + w, id0, q + G < nfull ? (q + G) * 4 + w : -1, lane, &o, pt, &idn,
+                      ids_lds);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   for (; q < nfull; q += G) {
     const int64_t c = q * 4 + w;
@@ -165,6 +183,14 @@ EvaluateGroupStorePipelined(const GroupArgs a, int64_t nfull) {
     const double cost = LossAndCorrect<K, kLoss, true>(a.loss, a.apply_loss, r, J0, J1, true);
     const double wsum = WaveSumLane0(cost);
     const bool failed = __ballot(!ok) != 0;
+    // the next quad's ids (landed with this quad's inputs), before the
+    // staging below overwrites the landing areas
+    {
+      const char* fb = reinterpret_cast<const char*>(fw);
+      const uint32_t ic = *reinterpret_cast<const uint32_t*>(fb + kPgsIdcOff + 4 * lane);
+      const uint32_t ip = *reinterpret_cast<const uint32_t*>(fb + kPgsIdpOff + 4 * lane);
+      idn = (long long)(((uint64_t)ip << 32) | ic);
+    }
     KeepAlive<13>(qv);  // the previous quad's stores may still be reading these
 #pragma unroll
     for (int k = 0; k < NR * S0; k += 2)
@@ -193,7 +219,7 @@ EvaluateGroupStorePipelined(const GroupArgs a, int64_t nfull) {
     const int64_t qn = q + G;
     if (qn < nfull)
       PgsIssueGather<K>(a, fw, qn * 4 + w, idn, qn + G < nfull ? (qn + G) * 4 + w : -1, lane, &on, ptn,
-                        &idnn);
+                        &idnn, ids_lds);
     const int64_t b0 = q * 4 * kWave;
     double* const bases[3] = {a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * b0,
                               a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * b0,
@@ -205,8 +231,7 @@ EvaluateGroupStorePipelined(const GroupArgs a, int64_t nfull) {
       default: PgsStores<3>(bases, voff, qv); break;
     }
     // the gather (older than the 13 stores) has landed
-    asm volatile("s_waitcnt vmcnt(13)" : "+v"(idnn) : : "memory");
-    idn = idnn;
+    asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
   }
   KeepAlive<13>(qv);
   asm volatile("" ::"v"(voff));
