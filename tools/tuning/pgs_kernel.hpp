@@ -101,27 +101,28 @@ __device__ __forceinline__ void PgsIssueGather(const GroupArgs& a, double* lds, 
     const double* src = a.packed0 + (int64_t)kRow * cid + 2 * qq;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(lbase + 2u * kWave * 8u * k);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
-                 : "memory");
+                 : "memory", "m0");
   }
   // The observation pair (16 B a lane) and the point (two 12-byte pieces a
   // lane) by LDS-DMA too, after the camera rows in the same region: no VGPR
   // holds them while they are in flight.
+  // (An LDS-DMA instruction's immediate offset moves its LDS destination
+  // too, so every source offset is in the address register, offset 0.)
   const double* po = a.data + 2 * (c * kWave + lane);
   const uint32_t mo = __builtin_amdgcn_readfirstlane(lbase + kPgsObsOff);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(po), "s"(mo)
-               : "memory");
+               : "memory", "m0");
   const double* pt = a.state + a.state_base[1] + 3LL * pid;
   const uint32_t mxy = __builtin_amdgcn_readfirstlane(lbase + kPgsXyOff);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(pt), "s"(mxy)
-               : "memory");
+               : "memory", "m0");
+  const char* pz = reinterpret_cast<const char*>(pt) + 16;
   const uint32_t mzl = __builtin_amdgcn_readfirstlane(lbase + kPgsZloOff);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off offset:16 nt" ::"v"(pt),
-               "s"(mzl)
-               : "memory");
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(pz), "s"(mzl)
+               : "memory", "m0");
   const uint32_t mzh = __builtin_amdgcn_readfirstlane(lbase + kPgsZhiOff);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off offset:20 nt" ::"v"(pt),
-               "s"(mzh)
-               : "memory");
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(pz + 4), "s"(mzh)
+               : "memory", "m0");
   (void)o;
   (void)p;
   (void)idn;
@@ -129,11 +130,10 @@ __device__ __forceinline__ void PgsIssueGather(const GroupArgs& a, double* lds, 
     const int32_t* pi = a.ids + 2 * (cn * kWave + lane);
     const uint32_t mic = __builtin_amdgcn_readfirstlane(ids_lds + kPgsIdcOff);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(pi), "s"(mic)
-                 : "memory");
+                 : "memory", "m0");
     const uint32_t mip = __builtin_amdgcn_readfirstlane(ids_lds + kPgsIdpOff);
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off offset:4 nt" ::"v"(pi),
-                 "s"(mip)
-                 : "memory");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(pi + 1), "s"(mip)
+                 : "memory", "m0");
   }
 }
 
