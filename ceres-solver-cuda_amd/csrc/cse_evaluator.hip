@@ -363,6 +363,17 @@ void LaunchPgs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 }
 
 template <class K, int L>
+void LaunchGroupStore2P(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  if (!cse::GroupStoreEligible(a)) {
+    LaunchTwoRound<K, L, 2>(a, num_wg, s);
+    return;
+  }
+  const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore2P<K, L>), dim3((unsigned)((chunks + 3) / 4)),
+                     dim3(4 * cse::kWave), 0, s, a);
+}
+
+template <class K, int L>
 void LaunchW1Only(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
   const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
@@ -671,6 +682,8 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 80: return &LaunchW1Only<K, L>;
     // the group-store kernel, persistent and software-pipelined
     case 88: return &LaunchPgs<K, L>;
+    // the group-store kernel staging in two phases (16 waves per CU)
+    case 89: return &LaunchGroupStore2P<K, L>;
     default: return nullptr;
   }
 }

@@ -184,6 +184,105 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
   }
 }
 
+// Tuning build: the same with the image staged in two phases through 36 KiB
+// (4 workgroups, 16 waves per CU): the F cells (each wave then stores its
+// own chunk's 9 KiB F segment), then E and residuals in the same LDS (wave
+// w < 3 stores a third of the E run, wave 3 the residuals).
+template <class K, int kLoss>
+__global__ __launch_bounds__(4 * kWave) __attribute__((amdgpu_waves_per_eu(4))) void
+EvaluateAffineChunksGroupStore2P(const GroupArgs a) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  static_assert(NR == 2 && S0 == 9 && S1 == 3, "Snavely-shaped kinds");
+  constexpr int kW = 4;
+  __shared__ __attribute__((aligned(16))) double img[kQuadFk * kW * 128];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t num_chunks = (a.n + kWave - 1) / kWave;
+  const int64_t c = (int64_t)blockIdx.x * kW + w;
+  const bool has = c < num_chunks;
+  const int64_t i0 = c * kWave;
+  const int64_t rem = a.n - i0;
+  const int nw = !has ? 0 : rem < kWave ? (int)rem : kWave;
+  const bool active = lane < nw;
+  const int64_t i = active ? i0 + lane : (a.n > 0 ? a.n - 1 : 0);
+  double* fw = img + w * (NR * S0 * kWave);
+  double r[NR], J0[NR * S0], J1[NR * S1p];
+  bool ok = true;
+  double cost = 0.0;
+  if (has) {
+    AffineInputs<K> in;
+    const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
+    GatherCoopDma<K>(a, i, make_int2((int)b, (int)(b >> 32)), &in, fw, lane);
+    ok = EvaluateFunctor<K, true>(in.d, in.x0, in.x1, r, J0, J1);
+    if (ok && a.check_finite)
+      ok = !(AnyNonFinite<NR>(r) || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1));
+    cost = LossAndCorrect<K, kLoss, true>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
+  }
+  const double wsum = WaveSumLane0(active ? cost : 0.0);
+  const bool failed = __ballot(active && !ok) != 0;
+  double* v_partial = a.partials + c;
+  const int64_t wg0 = (int64_t)blockIdx.x * kW * kWave;
+  double* fbase = a.jacobian ? a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * wg0 : nullptr;
+  double* ebase = a.jacobian ? a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * wg0 : nullptr;
+  double* rbase = a.residuals ? a.residuals + a.res_base + (int64_t)NR * wg0 : nullptr;
+  const bool full = wg0 + kW * kWave <= a.n;
+  const bool fast = full && fbase && rbase &&
+                    ((reinterpret_cast<uintptr_t>(fbase) | reinterpret_cast<uintptr_t>(ebase) |
+                      reinterpret_cast<uintptr_t>(rbase)) & 63) == 0;
+  if (fast) {
+    const double2* im2 = reinterpret_cast<const double2*>(img);
+    cse_v4i q[13];
+    // phase 1: the wave's own F cells, read back as its 9 KiB segment
+#pragma unroll
+    for (int k = 0; k < NR * S0; k += 2)
+      *reinterpret_cast<double2*>(fw + lane * NR * S0 + k) = make_double2(J0[k], J0[k + 1]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const double2 v = im2[(9 * w + j) * kWave + lane];
+      q[j] = AsV4i(v.x, v.y);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's F pieces are in registers
+    // phase 2: E cells [0, 12 KiB) and residuals [12, 16 KiB) of the workgroup
+#pragma unroll
+    for (int k = 0; k < NR * S1; k += 2)
+      *reinterpret_cast<double2*>(img + w * (NR * S1 * kWave) + lane * NR * S1 + k) =
+          make_double2(J1[k], J1[k + 1]);
+    *reinterpret_cast<double2*>(img + kQuadEk * kW * 128 + w * (NR * kWave) + lane * NR) =
+        make_double2(r[0], r[1]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double2 v = im2[(4 * w + j) * kWave + lane];
+      q[9 + j] = AsV4i(v.x, v.y);
+    }
+    double* f0 = fbase + 128 * 9 * w + 2 * lane + 512;
+    double* s0 = (w < 3 ? ebase + 128 * 4 * w : rbase) + 2 * lane + 512;
+    asm volatile("" : "+v"(v_partial));
+    double v_wsum = wsum;
+    asm volatile("" : "+v"(v_wsum));
+    asm volatile("" ::"v"(f0), "v"(s0));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    QuadRun<9, 0>(f0, q);
+    QuadRun<4, 9>(s0, q);
+    if (lane == 0) {
+      StoreB64(v_partial, v_wsum);
+      if (failed) StoreB32(a.status, 1);
+    }
+    KeepAlive<13>(q);
+    asm volatile("" ::"v"(f0), "v"(s0), "v"(v_partial), "v"(v_wsum));
+    return;
+  }
+  __syncthreads();
+  if (has) StageAndStore<K, true, false>(a, fw, lane, active, i0, nw, r, J0, J1);
+  if (lane == 0 && has) {
+    *v_partial = wsum;
+    if (failed) *a.status = 1;
+  }
+}
+
 // May the group take EvaluateAffineChunksGroupStore?  Both outputs, and the
 // residual, E-cell and F-cell bases on 64-byte sectors.
 inline bool GroupStoreEligible(const GroupArgs& a) {
