@@ -58,12 +58,24 @@ struct QuadPart {
   static constexpr int n(int r) { return (hi < re(r) ? hi : re(r)) - s(r) > 0 ? (hi < re(r) ? hi : re(r)) - s(r) : 0; }
 };
 
+// The fused gradient's per-wave stores (gradient_mode 0, points only): the
+// point rows that are this wave's alone and the two boundary entries
+// (FusedGrad), exec-masked, after the wave's runs.  Passed as values: a
+// struct handed down by pointer stayed in scratch (96 B a lane).
+struct GroupGradStores {
+  double* gp;
+  double* sp;
+  double g0, g1, g2;
+  cse_v4i sq0, sq1;
+  bool interior, writer;
+};
+
 // Read wave w's pieces from the workgroup image and store them, region by
 // region (at most three runs).
-template <int kW, int kSched, int w>
+template <int kW, int kSched, int w, bool kG>
 __device__ __forceinline__ void QuadTail(const double* img, double* const bases[3], int lane,
                                          double* v_partial, double v_wsum, bool failed,
-                                         int* status_dst) {
+                                         int* status_dst, GroupGradStores gs) {
   using P = QuadPart<kW, kSched, w>;
   constexpr int N = P::N;
   static_assert(N > 0 && N <= 24, "pieces per wave");
@@ -84,24 +96,36 @@ __device__ __forceinline__ void QuadTail(const double* img, double* const bases[
   QuadRun<P::n(0), 0>(b0, q);
   QuadRun<P::n(1), P::n(0)>(b1, q);
   QuadRun<P::n(2), P::n(0) + P::n(1)>(b2, q);
+  if constexpr (kG) {
+    if (gs.interior) {
+      StoreB64At<0>(gs.gp, gs.g0);
+      StoreB64At<8>(gs.gp, gs.g1);
+      StoreB64At<16>(gs.gp, gs.g2);
+    }
+    if (gs.writer) {
+      StoreNt16<0, 1>(gs.sp, gs.sq0);
+      StoreNt16<16, 1>(gs.sp, gs.sq1);
+    }
+  }
   if (lane == 0) {
     StoreB64(v_partial, v_wsum);
     if (failed) StoreB32(status_dst, 1);
   }
   KeepAlive<N>(q);
+  if constexpr (kG) asm volatile("" ::"v"(gs.gp), "v"(gs.sp), "v"(gs.g0), "v"(gs.g1), "v"(gs.g2), "v"(gs.sq0), "v"(gs.sq1));
   asm volatile("" ::"v"(b0), "v"(b1), "v"(b2), "v"(v_partial), "v"(v_wsum));
 }
 
-template <int kW, int kSched, int w = 0>
+template <int kW, int kSched, bool kG = false, int w = 0>
 __device__ __forceinline__ void QuadTailFor(int wave, const double* img, double* const bases[3], int lane,
                                             double* v_partial, double v_wsum, bool failed,
-                                            int* status_dst) {
+                                            int* status_dst, GroupGradStores gs = {}) {
   if constexpr (w < kW) {
     if (wave == w) {
-      QuadTail<kW, kSched, w>(img, bases, lane, v_partial, v_wsum, failed, status_dst);
+      QuadTail<kW, kSched, w, kG>(img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
       return;
     }
-    QuadTailFor<kW, kSched, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst);
+    QuadTailFor<kW, kSched, kG, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
   }
 }
 
@@ -109,7 +133,10 @@ __device__ __forceinline__ void QuadTailFor(int wave, const double* img, double*
 template <int kW, int kPadKiB>
 constexpr int kQuadWavesPerEu = ((160 / (13 * kW + kPadKiB)) * kW + 3) / 4;
 
-template <class K, int kLoss, int kW, int kSched, int kPadKiB>
+// kGradF: the fused gradient's points-only form (gradient_mode 0; the
+// slot-0 rows come from CameraGradientKernel), as
+// EvaluateAffineChunksFusedPointsW1.
+template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kGradF = false>
 __global__ __launch_bounds__(kW * kWave) __attribute__((amdgpu_waves_per_eu(kQuadWavesPerEu<kW, kPadKiB>))) void
 EvaluateAffineChunksGroupStore(const GroupArgs a) {
   using Tr = KindTraits<K>;
@@ -134,6 +161,7 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok = true;
   double cost = 0.0;
+  int id1 = 0;
   if (has) {
     AffineInputs<K> in;
     const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
@@ -143,14 +171,33 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
     if (ok && a.check_finite)
       ok = !(AnyNonFinite<NR>(r) || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1));
     cost = LossAndCorrect<K, kLoss, true>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
-    if (a.gradient != nullptr && active) {  // gradient_mode 2: FP64 atomics, as the reference
+    if (!kGradF && a.gradient != nullptr && active) {  // gradient_mode 2: FP64 atomics, as the reference
       AddGradientSlot<NR, S0>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0, S0, r, J0);
       AddGradientSlot<NR, S1p>(a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1, S1, r, J1);
     }
+    id1 = in.id1;
   }
   const double wsum = WaveSumLane0(active ? cost : 0.0);
   const bool failed = __ballot(active && !ok) != 0;
   double* v_partial = a.partials + c;
+  // The fused gradient's slot-1 (point) rows: per wave, as the one-wave
+  // points kernel (FusedGrad; exec-masked stores after the runs).
+  FusedGrad<K> fg;
+  GroupGradStores gs{};
+  if constexpr (kGradF) {
+    if (has) {
+      fg.Compute(r, J0, J1, id1, active, lane, nw, c);
+      gs.interior = fg.interior;
+      gs.writer = fg.writer;
+      gs.gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
+      gs.sp = a.gside + 4 * fg.entry;
+      gs.g0 = fg.g1[0];
+      gs.g1 = fg.g1[1];
+      gs.g2 = fg.g1[2];
+      gs.sq0 = AsV4i(fg.g1[0], fg.g1[1]);
+      gs.sq1 = AsV4i(fg.g1[2], fg.g1[3]);
+    }
+  }
 
   const int64_t wg0 = (int64_t)blockIdx.x * kW * kWave;  // the workgroup's first block
   double* fbase = a.jacobian ? a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * wg0 : nullptr;
@@ -171,13 +218,32 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
     *reinterpret_cast<double2*>(rw + lane * NR) = make_double2(r[0], r[1]);
     __syncthreads();
     double* const bases[3] = {fbase, ebase, rbase};
-    QuadTailFor<kW, kSched>(w, img, bases, lane, v_partial, wsum, failed, a.status);
+    QuadTailFor<kW, kSched, kGradF>(w, img, bases, lane, v_partial, wsum, failed, a.status, gs);
     return;
   }
   // The last (partial) workgroup or unaligned outputs: each wave its own
   // chunk through the slow tail, in its own F region.
   __syncthreads();  // every wave's gather landing area is free again
   if (has) StageAndStore<K, true, false>(a, fw, lane, active, i0, nw, r, J0, J1);
+  if constexpr (kGradF) {
+    if (has) {  // plain stores, as AffineChunkBody's slow tail
+      if (fg.interior) {
+        double* g = a.gfused + a.delta_base[1] + 3LL * fg.key;
+        g[0] = fg.g1[0];
+        g[1] = fg.g1[1];
+        g[2] = fg.g1[2];
+      }
+      if (fg.writer) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a.gside[4 * fg.entry + q] = fg.g1[q];
+      }
+      if (nw == 1 && lane == 0) {  // a one-block wave: its zero entry
+        double* e = a.gside + 4 * (2 * c + 1);
+        e[0] = e[1] = e[2] = 0.0;
+        e[3] = fg.g1[3];
+      }
+    }
+  }
   if (lane == 0 && has) {  // slots past the last chunk stay 0 (zeroed at cse_create)
     *v_partial = wsum;
     if (failed) *a.status = 1;
