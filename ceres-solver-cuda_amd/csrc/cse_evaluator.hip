@@ -457,8 +457,24 @@ void LaunchPersistent(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 #ifndef CSE_TWOROUNDCRS_W1
 #define CSE_TWOROUNDCRS_W1 1
 #endif
+// CSE_GROUP_STORE_CRS 1: the Snavely camera's CRS residual+Jacobian
+// evaluation on 64-byte sectors through the group-store kernel (48 KiB row
+// runs).  Measured slower than the one-wave CRS kernel at its 20 waves per
+// CU: problem-13682 1.470-1.474 against 1.429-1.431 ms, problem-1778
+// 0.283-0.288 against 0.263-0.267 ms (profiles/round5/r5k), so off.
+#ifndef CSE_GROUP_STORE_CRS
+#define CSE_GROUP_STORE_CRS 0
+#endif
 template <class K, int L, int Co, class T = cse::ShippedTune>
 void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
+  if constexpr (CSE_GROUP_STORE_CRS != 0 && kGroupStore<K, T> && Co == 2) {
+    if (cse::GroupStoreEligibleCrs(a)) {
+      const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
+      hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, 4, 0, 0, false, true>),
+                         dim3((unsigned)((chunks + 3) / 4)), dim3(4 * cse::kWave), 0, s, a);
+      return;
+    }
+  }
   if constexpr (CSE_TWOROUNDCRS_W1 != 0 || T::kConst0) {
     const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksTwoRoundCrsW1<K, L, Co, T>), dim3((unsigned)chunks),
@@ -919,6 +935,12 @@ int Validate(const cse_problem_desc* d) {
 #ifndef CSE_CAMGRAD_PASS_MB
 #define CSE_CAMGRAD_PASS_MB 96
 #endif
+// The camera sums over written contributions (gradient_mode 3, the Schur
+// and CGNR operators' F^T u) take the same plan's chunks pass-major too
+// (GradientContribKernel's order; 0: chunk order, camera-major).
+#ifndef CSE_CONTRIB_PASS_ORDER
+#define CSE_CONTRIB_PASS_ORDER 1
+#endif
 int CamGradPasses(const cse_residual_group& g, const KindShape& k) {
   int32_t lo = INT32_MAX, hi = INT32_MIN;
   for (int64_t i = 0; i < g.num_blocks; ++i) {
@@ -1348,7 +1370,8 @@ int LaunchFusedGradTail(const Group& G, double* out, hipStream_t s) {
   if (P.nchunks > 0)
     hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
                        dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
-                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch);
+                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch,
+                       CSE_CONTRIB_PASS_ORDER ? P.chunk_order.p : nullptr);
   hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
                      dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, ga, ch);
@@ -2350,7 +2373,8 @@ int SchurFTail(cse_evaluator* ev, double* y, hipStream_t s) {
   if (P.nchunks > 0)
     hipLaunchKernelGGL((cse::GradientContribKernel<9, 10>),
                        dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
-                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch);
+                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch,
+                       CSE_CONTRIB_PASS_ORDER ? P.chunk_order.p : nullptr);
   hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
                      dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, ga, ch);

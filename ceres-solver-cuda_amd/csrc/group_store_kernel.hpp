@@ -24,7 +24,10 @@
 // outputs are requested; otherwise the one-wave kernel, whose sector-window
 // tail handles any alignment.  The last, partial workgroup stores each
 // chunk through the slow tail.  Gradient atomics (gradient_mode 2) as the
-// one-wave kernel.
+// one-wave kernel.  Two more forms are built only on request, each measured
+// slower than the one-wave kernel it would replace: the
+// fused gradient's points form (kGradF, -DCSE_GROUP_STORE_FP=1) and the
+// CompressedRowSparseMatrix form (kCrs, -DCSE_GROUP_STORE_CRS=1).
 #ifndef CSE_GROUP_STORE_KERNEL_HPP_
 #define CSE_GROUP_STORE_KERNEL_HPP_
 
@@ -43,10 +46,11 @@ __device__ __forceinline__ void QuadRun(double* base, const cse_v4i* q) {
   if constexpr (N > 0) SegmentStoresFrom<0, N>(base, base + 1024, q + J0);
 }
 
-// Wave w's part of the workgroup image [F | E | R] (KiB): [lo, hi).
-template <int kW, int kSched, int w>
+// Wave w's part of the workgroup image [F | E | R] (KiB): [lo, hi).  The
+// CompressedRowSparseMatrix form has one Jacobian region: kFk = 12, kEk = 0.
+template <int kW, int kSched, int w, int kFk = kQuadFk, int kEk = kQuadEk>
 struct QuadPart {
-  static constexpr int F = kQuadFk * kW, E = kQuadEk * kW, R = kQuadRk * kW;
+  static constexpr int F = kFk * kW, E = kEk * kW, R = kQuadRk * kW;
   static constexpr int T = F + E + R;
   static constexpr int lo = kSched == 1 ? (w < 3 ? w * F / 3 : F) : T * w / kW;
   static constexpr int hi = kSched == 1 ? (w < 3 ? (w + 1) * F / 3 : T) : T * (w + 1) / kW;
@@ -72,11 +76,11 @@ struct GroupGradStores {
 
 // Read wave w's pieces from the workgroup image and store them, region by
 // region (at most three runs).
-template <int kW, int kSched, int w, bool kG>
+template <int kW, int kSched, int w, bool kG, int kFk, int kEk>
 __device__ __forceinline__ void QuadTail(const double* img, double* const bases[3], int lane,
                                          double* v_partial, double v_wsum, bool failed,
                                          int* status_dst, GroupGradStores gs) {
-  using P = QuadPart<kW, kSched, w>;
+  using P = QuadPart<kW, kSched, w, kFk, kEk>;
   constexpr int N = P::N;
   static_assert(N > 0 && N <= 24, "pieces per wave");
   cse_v4i q[N];
@@ -116,16 +120,17 @@ __device__ __forceinline__ void QuadTail(const double* img, double* const bases[
   asm volatile("" ::"v"(b0), "v"(b1), "v"(b2), "v"(v_partial), "v"(v_wsum));
 }
 
-template <int kW, int kSched, bool kG = false, int w = 0>
+template <int kW, int kSched, bool kG = false, int kFk = kQuadFk, int kEk = kQuadEk, int w = 0>
 __device__ __forceinline__ void QuadTailFor(int wave, const double* img, double* const bases[3], int lane,
                                             double* v_partial, double v_wsum, bool failed,
                                             int* status_dst, GroupGradStores gs = {}) {
   if constexpr (w < kW) {
     if (wave == w) {
-      QuadTail<kW, kSched, w, kG>(img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
+      QuadTail<kW, kSched, w, kG, kFk, kEk>(img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
       return;
     }
-    QuadTailFor<kW, kSched, kG, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
+    QuadTailFor<kW, kSched, kG, kFk, kEk, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst,
+                                                 gs);
   }
 }
 
@@ -136,12 +141,21 @@ constexpr int kQuadWavesPerEu = ((160 / (13 * kW + kPadKiB)) * kW + 3) / 4;
 // kGradF: the fused gradient's points-only form (gradient_mode 0; the
 // slot-0 rows come from CameraGradientKernel), as
 // EvaluateAffineChunksFusedPointsW1.
-template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kGradF = false>
+// kCrs: CompressedRowSparseMatrix values (block_jacobian_writer's CRS
+// sibling, compressed_row_jacobian_writer.cc): a block's NR rows of N = 12
+// columns are contiguous, so a workgroup's four chunks own one 48 KiB run of
+// rows and one 4 KiB run of residuals; each lane stages its rows with the
+// group's column offsets (camera and point columns in either order).
+template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kGradF = false, bool kCrs = false>
 __global__ __launch_bounds__(kW * kWave) __attribute__((amdgpu_waves_per_eu(kQuadWavesPerEu<kW, kPadKiB>))) void
 EvaluateAffineChunksGroupStore(const GroupArgs a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
+  constexpr int N = S0 + S1;
   static_assert(NR == 2 && S0 == 9 && S1 == 3, "Snavely-shaped kinds");
+  static_assert(!(kCrs && kGradF), "the fused gradient is a BlockSparseMatrix form");
+  // KiB per chunk of the Jacobian regions: BSM F 9 and E 3, CRS rows 12
+  constexpr int kFk = kCrs ? kQuadFk + kQuadEk : kQuadFk, kEk = kCrs ? 0 : kQuadEk;
   constexpr int kImg = (13 * kW + kPadKiB) * 128;  // doubles
   __shared__ __attribute__((aligned(16))) double img[kImg];
   const int lane = threadIdx.x & (kWave - 1);
@@ -154,9 +168,9 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
   const int nw = !has ? 0 : rem < kWave ? (int)rem : kWave;
   const bool active = lane < nw;
   const int64_t i = active ? i0 + lane : (a.n > 0 ? a.n - 1 : 0);
-  double* fw = img + w * (NR * S0 * kWave);  // this wave's F cells (and its gather landing area)
-  double* ew = img + kQuadFk * kW * 128 + w * (NR * S1 * kWave);
-  double* rw = img + (kQuadFk + kQuadEk) * kW * 128 + w * (NR * kWave);
+  double* fw = img + w * (kFk * 128);  // this wave's F cells or rows (and its gather landing area)
+  double* ew = img + kFk * kW * 128 + w * (NR * S1 * kWave);
+  double* rw = img + (kFk + kEk) * kW * 128 + w * (NR * kWave);
 
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok = true;
@@ -200,8 +214,12 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
   }
 
   const int64_t wg0 = (int64_t)blockIdx.x * kW * kWave;  // the workgroup's first block
-  double* fbase = a.jacobian ? a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * wg0 : nullptr;
-  double* ebase = a.jacobian ? a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * wg0 : nullptr;
+  // CRS: the first row's offset (the slots' first columns, either order)
+  const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
+  double* fbase = !a.jacobian ? nullptr
+                  : kCrs      ? a.jacobian + row0 + (int64_t)NR * N * wg0
+                              : a.jacobian + a.jac_base[0][0] + a.jac_stride[0] * wg0;
+  double* ebase = kCrs || !a.jacobian ? fbase : a.jacobian + a.jac_base[1][0] + a.jac_stride[1] * wg0;
   double* rbase = a.residuals ? a.residuals + a.res_base + (int64_t)NR * wg0 : nullptr;
   const bool full = wg0 + kW * kWave <= a.n;
   const bool fast = full && fbase && rbase &&
@@ -209,22 +227,34 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
                       reinterpret_cast<uintptr_t>(rbase)) & 63) == 0;
   if (fast) {
     // Stage the wave's cells in output order (every lane active here).
+    if constexpr (kCrs) {
+      double* row = fw + lane * NR * N;
 #pragma unroll
-    for (int q = 0; q < NR * S0; q += 2)
-      *reinterpret_cast<double2*>(fw + lane * NR * S0 + q) = make_double2(J0[q], J0[q + 1]);
+      for (int k = 0; k < NR; ++k) {
+        const int c0 = (int)(a.jac_base[0][k] - row0), c1 = (int)(a.jac_base[1][k] - row0);
 #pragma unroll
-    for (int q = 0; q < NR * S1; q += 2)
-      *reinterpret_cast<double2*>(ew + lane * NR * S1 + q) = make_double2(J1[q], J1[q + 1]);
+        for (int cc = 0; cc < S0; ++cc) row[c0 + cc] = J0[k * S0 + cc];
+#pragma unroll
+        for (int cc = 0; cc < S1; ++cc) row[c1 + cc] = J1[k * S1p + cc];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NR * S0; q += 2)
+        *reinterpret_cast<double2*>(fw + lane * NR * S0 + q) = make_double2(J0[q], J0[q + 1]);
+#pragma unroll
+      for (int q = 0; q < NR * S1; q += 2)
+        *reinterpret_cast<double2*>(ew + lane * NR * S1 + q) = make_double2(J1[q], J1[q + 1]);
+    }
     *reinterpret_cast<double2*>(rw + lane * NR) = make_double2(r[0], r[1]);
     __syncthreads();
     double* const bases[3] = {fbase, ebase, rbase};
-    QuadTailFor<kW, kSched, kGradF>(w, img, bases, lane, v_partial, wsum, failed, a.status, gs);
+    QuadTailFor<kW, kSched, kGradF, kFk, kEk>(w, img, bases, lane, v_partial, wsum, failed, a.status, gs);
     return;
   }
   // The last (partial) workgroup or unaligned outputs: each wave its own
-  // chunk through the slow tail, in its own F region.
+  // chunk through the slow tail, in its own F region (CRS: its 12 KiB of rows).
   __syncthreads();  // every wave's gather landing area is free again
-  if (has) StageAndStore<K, true, false>(a, fw, lane, active, i0, nw, r, J0, J1);
+  if (has) StageAndStore<K, true, kCrs>(a, fw, lane, active, i0, nw, r, J0, J1);
   if constexpr (kGradF) {
     if (has) {  // plain stores, as AffineChunkBody's slow tail
       if (fg.interior) {
@@ -351,6 +381,16 @@ EvaluateAffineChunksGroupStore2P(const GroupArgs a) {
 
 // May the group take EvaluateAffineChunksGroupStore?  Both outputs, and the
 // residual, E-cell and F-cell bases on 64-byte sectors.
+// CRS: the residuals and the group's first row on 64-byte sectors (a block's
+// NR x N rows are contiguous on the affine CRS path).
+inline bool GroupStoreEligibleCrs(const GroupArgs& a) {
+  if (!a.residuals || !a.jacobian) return false;
+  const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
+  const uintptr_t m = reinterpret_cast<uintptr_t>(a.residuals + a.res_base) |
+                      reinterpret_cast<uintptr_t>(a.jacobian + row0);
+  return (m & 63) == 0;
+}
+
 inline bool GroupStoreEligible(const GroupArgs& a) {
   if (!a.residuals || !a.jacobian) return false;
   const uintptr_t m = reinterpret_cast<uintptr_t>(a.residuals + a.res_base) |

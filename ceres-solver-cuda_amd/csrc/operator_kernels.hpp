@@ -156,14 +156,19 @@ __global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const
 // block list sums the blocks' written contributions (S of the SP doubles
 // per block; two 64-byte sectors per block instead of the Jacobian cell
 // and residual pair), a fixed butterfly, then GradientChunkReduceKernel.
+// order (may be null): the chunks taken pass-major (BuildGradPlan), so the
+// resident waves read the records of one block range at a time and the
+// 64-byte sectors two neighbouring 80-byte records share are fetched once.
 template <int S, int SP>
 __global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const double* contrib,
                                                                        const int32_t* perm,
-                                                                       const GradChunks ch) {
+                                                                       const GradChunks ch,
+                                                                       const int32_t* order) {
   static_assert(SP % 2 == 0 && SP >= S, "16-byte records");
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  if (cid >= ch.nchunks) return;
+  const int64_t slot = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (slot >= ch.nchunks) return;
+  const int64_t cid = order ? (int64_t)order[slot] : slot;
   const int64_t q1 = ch.begin[cid + 1];
   double acc[S];
 #pragma unroll
