@@ -430,11 +430,11 @@ void LaunchTwoRoundProbe(const cse::GroupArgs& a0, int64_t num_wg, hipStream_t s
 
 // Tuning build: kW-wave workgroups storing their kW chunks' outputs as long
 // runs (group_store_kernel.hpp; the product launches kW = 4).  Variants 90-98.
-template <class K, int L, int kW, int kSched, int kPad = 0>
+template <class K, int L, int kW, int kSched, int kPad = 0, int kVm = 0>
 void LaunchQuad(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
   const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad>), dim3((unsigned)((chunks + kW - 1) / kW)),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad, false, false, kVm>), dim3((unsigned)((chunks + kW - 1) / kW)),
                      dim3(kW * cse::kWave), 0, s, a);
 }
 
@@ -718,6 +718,11 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 88: return &LaunchPgs<K, L>;
     // the group-store kernel staging in two phases (16 waves per CU)
     case 89: return &LaunchGroupStore2P<K, L>;
+    // the group-store kernel with at most 1 / 2 / 4 / 8 of a wave's stores in flight
+    case 100: return &LaunchQuad<K, L, 4, 0, 0, 1>;
+    case 101: return &LaunchQuad<K, L, 4, 0, 0, 2>;
+    case 102: return &LaunchQuad<K, L, 4, 0, 0, 4>;
+    case 103: return &LaunchQuad<K, L, 4, 0, 0, 8>;
     default: return nullptr;
   }
 }

@@ -46,6 +46,18 @@ __device__ __forceinline__ void QuadRun(double* base, const cse_v4i* q) {
   if constexpr (N > 0) SegmentStoresFrom<0, N>(base, base + 1024, q + J0);
 }
 
+// Tuning build (kVm > 0): the same run with at most kVm of the wave's
+// stores in flight (s_waitcnt vmcnt after each store past the kVm-th), so
+// that a CU's memory queue holds fewer stores ahead of other waves' loads.
+template <int kVm, int kJ, int kCount, int kDone>
+__device__ __forceinline__ void QuadRunThrottled(double* b0, double* b1, const cse_v4i* q) {
+  if constexpr (kJ < kCount) {
+    StoreNt16<(kJ % 8) * 1024 - 4096, 0>(kJ < 8 ? b0 : b1, q[kJ]);
+    if constexpr (kDone + kJ + 1 > kVm) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kVm) : "memory");
+    QuadRunThrottled<kVm, kJ + 1, kCount, kDone>(b0, b1, q);
+  }
+}
+
 // Wave w's part of the workgroup image [F | E | R] (KiB): [lo, hi).  The
 // CompressedRowSparseMatrix form has one Jacobian region: kFk = 12, kEk = 0.
 template <int kW, int kSched, int w, int kFk = kQuadFk, int kEk = kQuadEk>
@@ -76,7 +88,7 @@ struct GroupGradStores {
 
 // Read wave w's pieces from the workgroup image and store them, region by
 // region (at most three runs).
-template <int kW, int kSched, int w, bool kG, int kFk, int kEk>
+template <int kW, int kSched, int w, bool kG, int kFk, int kEk, int kVm>
 __device__ __forceinline__ void QuadTail(const double* img, double* const bases[3], int lane,
                                          double* v_partial, double v_wsum, bool failed,
                                          int* status_dst, GroupGradStores gs) {
@@ -97,9 +109,15 @@ __device__ __forceinline__ void QuadTail(const double* img, double* const bases[
   asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
   asm volatile("" ::"v"(b0), "v"(b1), "v"(b2));
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  QuadRun<P::n(0), 0>(b0, q);
-  QuadRun<P::n(1), P::n(0)>(b1, q);
-  QuadRun<P::n(2), P::n(0) + P::n(1)>(b2, q);
+  if constexpr (kVm > 0) {
+    QuadRunThrottled<kVm, 0, P::n(0), 0>(b0, b0 + 1024, q);
+    QuadRunThrottled<kVm, 0, P::n(1), P::n(0)>(b1, b1 + 1024, q + P::n(0));
+    QuadRunThrottled<kVm, 0, P::n(2), P::n(0) + P::n(1)>(b2, b2 + 1024, q + P::n(0) + P::n(1));
+  } else {
+    QuadRun<P::n(0), 0>(b0, q);
+    QuadRun<P::n(1), P::n(0)>(b1, q);
+    QuadRun<P::n(2), P::n(0) + P::n(1)>(b2, q);
+  }
   if constexpr (kG) {
     if (gs.interior) {
       StoreB64At<0>(gs.gp, gs.g0);
@@ -120,16 +138,16 @@ __device__ __forceinline__ void QuadTail(const double* img, double* const bases[
   asm volatile("" ::"v"(b0), "v"(b1), "v"(b2), "v"(v_partial), "v"(v_wsum));
 }
 
-template <int kW, int kSched, bool kG = false, int kFk = kQuadFk, int kEk = kQuadEk, int w = 0>
+template <int kW, int kSched, bool kG = false, int kFk = kQuadFk, int kEk = kQuadEk, int kVm = 0, int w = 0>
 __device__ __forceinline__ void QuadTailFor(int wave, const double* img, double* const bases[3], int lane,
                                             double* v_partial, double v_wsum, bool failed,
                                             int* status_dst, GroupGradStores gs = {}) {
   if constexpr (w < kW) {
     if (wave == w) {
-      QuadTail<kW, kSched, w, kG, kFk, kEk>(img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
+      QuadTail<kW, kSched, w, kG, kFk, kEk, kVm>(img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
       return;
     }
-    QuadTailFor<kW, kSched, kG, kFk, kEk, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst,
+    QuadTailFor<kW, kSched, kG, kFk, kEk, kVm, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst,
                                                  gs);
   }
 }
@@ -146,7 +164,8 @@ constexpr int kQuadWavesPerEu = ((160 / (13 * kW + kPadKiB)) * kW + 3) / 4;
 // columns are contiguous, so a workgroup's four chunks own one 48 KiB run of
 // rows and one 4 KiB run of residuals; each lane stages its rows with the
 // group's column offsets (camera and point columns in either order).
-template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kGradF = false, bool kCrs = false>
+template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kGradF = false, bool kCrs = false,
+          int kVm = 0>
 __global__ __launch_bounds__(kW * kWave) __attribute__((amdgpu_waves_per_eu(kQuadWavesPerEu<kW, kPadKiB>))) void
 EvaluateAffineChunksGroupStore(const GroupArgs a) {
   using Tr = KindTraits<K>;
@@ -248,7 +267,7 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
     *reinterpret_cast<double2*>(rw + lane * NR) = make_double2(r[0], r[1]);
     __syncthreads();
     double* const bases[3] = {fbase, ebase, rbase};
-    QuadTailFor<kW, kSched, kGradF, kFk, kEk>(w, img, bases, lane, v_partial, wsum, failed, a.status, gs);
+    QuadTailFor<kW, kSched, kGradF, kFk, kEk, kVm>(w, img, bases, lane, v_partial, wsum, failed, a.status, gs);
     return;
   }
   // The last (partial) workgroup or unaligned outputs: each wave its own

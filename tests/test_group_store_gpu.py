@@ -36,8 +36,8 @@ LOSSES = [None, ca.Loss.huber(1.0), ca.Loss.cauchy(2.0)]
 
 
 def _prog(n, loss, seed=11):
-    cams = max(2, min(40, n // 8 + 2))
-    pts = max(2, n // 5 + 1)
+    cams = max(6, min(40, n // 8 + 2))
+    pts = max(1, min(n, n // 5 + 1))
     return bal.synthetic_program((cams, pts, n), loss=loss, format=ca.BLOCK_SPARSE, seed=seed)
 
 
