@@ -208,7 +208,13 @@ struct Group {
     DevBuf<double> chunk_partial;
     int64_t nchunks = 0;
     int64_t nperm = 0;  // blocks in the plan (all but those with a constant block)
+    bool all_present = false;  // every id in [lo, lo + count) has a block
   } grad[2];
+  // Gradient mode 0 writes every gradient row exactly once (grad_exact): one
+  // group, no constant blocks, every camera and point id of its ranges
+  // present and their rows tiling the effective parameters.  Then the tail
+  // kernels assign instead of adding and the gradient is not zeroed first.
+  bool grad_exact = false;
   // Constant slot-0 blocks on the affine path (BlockSparseMatrix): the
   // active-bit table over the slot-0 id range, each id's repack source
   // (state offset, or -1 - constant-state offset), and per 64-block chunk
@@ -946,6 +952,9 @@ int Validate(const cse_problem_desc* d) {
 #ifndef CSE_CONTRIB_PASS_ORDER
 #define CSE_CONTRIB_PASS_ORDER 1
 #endif
+#ifndef CSE_GRAD_ASSIGN
+#define CSE_GRAD_ASSIGN 1
+#endif
 int CamGradPasses(const cse_residual_group& g, const KindShape& k) {
   int32_t lo = INT32_MAX, hi = INT32_MIN;
   for (int64_t i = 0; i < g.num_blocks; ++i) {
@@ -1002,6 +1011,8 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
   for (int64_t p = 0; p < count * passes; ++p) poff[p + 1] += poff[p];
   std::vector<int64_t> off(count + 1);
   for (int64_t p = 0; p <= count; ++p) off[p] = poff[p * passes];
+  plan->all_present = true;
+  for (int64_t p = 0; p < count && plan->all_present; ++p) plan->all_present = off[p + 1] > off[p];
   int rc;
   if (!sorted) {
     std::vector<int32_t> perm(std::max<int64_t>(kept, 1));
@@ -1470,12 +1481,17 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
 
 // After the points kernel and CameraGradientKernel: the slot-1 boundary
 // entries, then the slot-0 rows from the chunk sums, in a fixed order.
-int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s) {
+// assign (grad_exact): the rows are written, not added to.
+int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s, bool assign = false) {
   const Group::GradPlan& P = G.grad[0];
   const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
-  hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>),
-                     dim3((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                     dim3(cse::kBlockThreads), 0, s, G.gside.p, entries, out, G.delta_base[1]);
+  const dim3 bgrid((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads));
+  if (assign)
+    hipLaunchKernelGGL((cse::GradientBoundaryKernel<3, true>), bgrid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
+                       entries, out, G.delta_base[1]);
+  else
+    hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>), bgrid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
+                       entries, out, G.delta_base[1]);
   cse::GradArgs ga{};
   ga.count = P.count;
   ga.lo = P.lo;
@@ -1483,9 +1499,11 @@ int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s) {
   ga.delta_base = G.delta_base[0];
   ga.delta_tab = G.const0 ? G.delta0.p + (P.lo - G.slot0_lo) : nullptr;
   const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
-  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
-                     dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                     dim3(cse::kBlockThreads), 0, s, ga, ch);
+  const dim3 cgrid((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads));
+  if (assign)
+    hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9, true>), cgrid, dim3(cse::kBlockThreads), 0, s, ga, ch);
+  else
+    hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), cgrid, dim3(cse::kBlockThreads), 0, s, ga, ch);
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }
@@ -1612,7 +1630,13 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       if (rc) return rc;
     }
   }
-  if (d_grad && ev->num_effective > 0)
+  // Gradient mode 0 over one grad_exact group (the fused points kernel, the
+  // camera rows and the boundary rows write every row once): no zeroing
+  // pass (CSE_GRAD_ASSIGN 0 keeps it, and the tail kernels add).
+  const bool grad_assign = CSE_GRAD_ASSIGN != 0 && d_grad && d_res && d_jac && ev->groups.size() == 1 &&
+                           ev->groups[0].grad_exact && ev->opts.gradient_mode == 0 &&
+                           ev->groups[0].grad[0].ready && ev->groups[0].grad[1].ready;
+  if (d_grad && ev->num_effective > 0 && !grad_assign)
     CSE_HIP(hipMemsetAsync(d_grad, 0, ev->num_effective * sizeof(double), ev->stream));
   if (d_jac && !ev->jac_covered && ev->num_jacobian_values > 0)
     CSE_HIP(hipMemsetAsync(d_jac, 0, ev->num_jacobian_values * sizeof(double), ev->stream));
@@ -1714,7 +1738,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       } else if ((rc = LaunchCameraGradKernel(ev, G, d_state, ev->stream))) {
         return rc;
       }
-      if ((rc = LaunchCameraGradReduce(G, d_grad, ev->stream))) return rc;
+      if ((rc = LaunchCameraGradReduce(G, d_grad, ev->stream, grad_assign))) return rc;
     } else if (fused) {
       const int rc = LaunchFusedGradTail(G, d_grad, ev->stream);
       if (rc) return rc;
@@ -2051,6 +2075,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     for (int64_t i = 0; ok && i < g.num_blocks; ++i)
       ok = owner[g.parameter_block_ids[2 * i + 1]] == 2 * gi + 1;
     G.fuse_ok = ok;
+    G.grad_exact = ok && ev->groups.size() == 1 && d->num_groups == 1 && !G.const0 &&
+                   ev->num_constant == 0 && G.shape.s0 == 9 && G.shape.s1 == 3 &&
+                   G.grad[0].all_present && G.grad[1].all_present &&
+                   9 * G.grad[0].count + 3 * G.grad[1].count == ev->num_effective;
   }
   if ((rc = BuildSchurPlan(ev, d, s))) return bail(rc);
   ev->res_covered = covered_res == d->num_residuals;

@@ -134,13 +134,15 @@ __global__ __launch_bounds__(kBlockThreads) void GradientLanesKernel(const GradA
   }
 }
 
-template <int S>
+// kAssign: the row is written, not added to (the evaluator's grad_exact:
+// every row of the gradient is written once and it is not zeroed first).
+template <int S, bool kAssign = false>
 __global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const GradArgs g,
                                                                            const GradChunks ch) {
   const int64_t p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
   if (p >= g.count) return;
   // A block without chunks adds nothing (and a constant one has no row).
-  if (ch.chunk_off[p] == ch.chunk_off[p + 1]) return;
+  if (!kAssign && ch.chunk_off[p] == ch.chunk_off[p + 1]) return;
   double acc[S];
 #pragma unroll
   for (int c = 0; c < S; ++c) acc[c] = 0.0;
@@ -149,7 +151,12 @@ __global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const
     for (int c = 0; c < S; ++c) acc[c] += ch.partial[q * S + c];
   double* dst = g.grad + (g.delta_tab ? g.delta_tab[p] : g.delta_base + (int64_t)S * (g.lo + p));
 #pragma unroll
-  for (int c = 0; c < S; ++c) dst[c] += acc[c];
+  for (int c = 0; c < S; ++c) {
+    if (kAssign)
+      dst[c] = acc[c];
+    else
+      dst[c] += acc[c];
+  }
 }
 
 // Fused-gradient slot 0 (FusedGrad): each chunk of a parameter block's
@@ -196,7 +203,7 @@ __global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const dou
 // wave order, so their ids are non-decreasing; the first entry of each id
 // adds that id's entries in order and adds the sum to the row (no interior
 // run of any wave touched these rows).
-template <int S>
+template <int S, bool kAssign = false>
 __global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const double* side,
                                                                         int64_t count,
                                                                         double* grad,
@@ -204,17 +211,55 @@ __global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const do
   static_assert(S <= 3, "entries hold 3 sums and the id");
   const int64_t e = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
   if (e >= count) return;
-  const double key = side[4 * e + 3];
-  if (e > 0 && side[4 * (e - 1) + 3] == key) return;
+  // The entry, its predecessor's id and the next two entries in one round
+  // trip (independent 16-byte loads; a key's entries are one to three in
+  // practice: a point continued from the previous wave, and into the next),
+  // then the rare longer runs entry by entry.  Summed in entry order from 0.
+  const double2* s2 = reinterpret_cast<const double2*>(side);
+  const double2 m0 = s2[2 * e], m1 = s2[2 * e + 1];
+  const double kprev = e > 0 ? side[4 * (e - 1) + 3] : -1.0;
+  double2 n0[2], n1[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int64_t f = e + 1 + t < count ? e + 1 + t : e;
+    n0[t] = s2[2 * f];
+    n1[t] = s2[2 * f + 1];
+  }
+  const double key = m1.y;
+  if (e > 0 && kprev == key) return;
   double acc[S];
 #pragma unroll
   for (int c = 0; c < S; ++c) acc[c] = 0.0;
-  for (int64_t f = e; f < count && side[4 * f + 3] == key; ++f)
+  auto add = [&](const double2& v0, const double2& v1) {
+    const double v[3] = {v0.x, v0.y, v1.x};
 #pragma unroll
-    for (int c = 0; c < S; ++c) acc[c] += side[4 * f + c];
+    for (int c = 0; c < S; ++c) acc[c] += v[c];
+  };
+  add(m0, m1);
+  int64_t f = e + 1;
+  bool more = true;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (more && f < count && n1[t].y == key) {
+      add(n0[t], n1[t]);
+      ++f;
+    } else {
+      more = false;
+    }
+  }
+  if (more) {
+    for (; f < count && side[4 * f + 3] == key; ++f)
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[c] += side[4 * f + c];
+  }
   double* dst = grad + delta_base + (int64_t)S * (int64_t)key;
 #pragma unroll
-  for (int c = 0; c < S; ++c) dst[c] += acc[c];
+  for (int c = 0; c < S; ++c) {
+    if (kAssign)
+      dst[c] = acc[c];
+    else
+      dst[c] += acc[c];
+  }
 }
 
 // Identity order (the points of a Schur-ordered problem): one 64-thread
