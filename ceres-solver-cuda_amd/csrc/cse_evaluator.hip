@@ -440,7 +440,7 @@ template <class K, int L, int kW, int kSched, int kPad = 0, int kVm = 0>
 void LaunchQuad(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
   const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad, false, false, kVm>), dim3((unsigned)((chunks + kW - 1) / kW)),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad, false, kVm>), dim3((unsigned)((chunks + kW - 1) / kW)),
                      dim3(kW * cse::kWave), 0, s, a);
 }
 
@@ -476,7 +476,7 @@ void LaunchTwoRoundCrs(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   if constexpr (CSE_GROUP_STORE_CRS != 0 && kGroupStore<K, T> && Co == 2) {
     if (cse::GroupStoreEligibleCrs(a)) {
       const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-      hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, 4, 0, 0, false, true>),
+      hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, 4, 0, 0, true>),
                          dim3((unsigned)((chunks + 3) / 4)), dim3(4 * cse::kWave), 0, s, a);
       return;
     }
@@ -502,26 +502,8 @@ void LaunchFused(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
 #ifndef CSE_FUSEDPOINTS_W1
 #define CSE_FUSEDPOINTS_W1 1
 #endif
-// The group-store kernel for the fused gradient's points form too
-// (kGradF): measured 2.069-2.073 against 2.017-2.019 ms per gradient
-// evaluation (profiles/round5/r5j), so off; the one-wave points kernel's
-// residuals-E-F tail order stays.
-#ifndef CSE_GROUP_STORE_FP
-#define CSE_GROUP_STORE_FP 0
-#endif
 template <class K, int L, bool Crs, class T = cse::PointsOnlyTune>
 void LaunchFusedPoints(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
-  // -DCSE_GROUP_STORE_FP=1: the Snavely camera's BSM form on 64-byte sectors
-  // through the group-store kernel with the fused point rows (2.6 % slower).
-  if constexpr (CSE_GROUP_STORE_FP != 0 && !Crs && std::is_same<K, cse::SnavelyKind>::value &&
-                std::is_same<T, cse::PointsOnlyTune>::value && CSE_BY_HAND != 0) {
-    if (cse::GroupStoreEligible(a)) {
-      const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-      hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, 4, 0, 0, true>),
-                         dim3((unsigned)((chunks + 3) / 4)), dim3(4 * cse::kWave), 0, s, a);
-      return;
-    }
-  }
   if constexpr (CSE_FUSEDPOINTS_W1 != 0) {
     const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
     hipLaunchKernelGGL((cse::EvaluateAffineChunksFusedPointsW1<K, L, Crs, T>), dim3((unsigned)chunks),

@@ -398,8 +398,7 @@ struct FusedGrad {
   __device__ __forceinline__ void Compute(const double* r, const double* J0, const double* J1,
                                           int id1, bool active, int lane, int nw, int64_t c) {
     using Tr = KindTraits<K>;
-    constexpr int NR = Tr::NR, S1p = Tr::S1p;
-    static_assert(Tr::NB == 2 && S1 == 3, "fused gradient: two slots, the second of size 3");
+    constexpr int NR = Tr::NR;
 #pragma unroll
     for (int cc = 0; cc < S0p; ++cc) {
       double s = 0.0;
@@ -409,6 +408,15 @@ struct FusedGrad {
       }
       g0[cc] = s;
     }
+    ComputePoints(r, J1, id1, active, lane, nw, c);
+  }
+
+  // The slot-1 (point) part alone (g0 untouched).
+  __device__ __forceinline__ void ComputePoints(const double* r, const double* J1, int id1, bool active,
+                                                int lane, int nw, int64_t c) {
+    using Tr = KindTraits<K>;
+    constexpr int NR = Tr::NR, S1p = Tr::S1p;
+    static_assert(Tr::NB == 2 && S1 == 3, "fused gradient: two slots, the second of size 3");
 #pragma unroll
     for (int cc = 0; cc < S1; ++cc) {
       double s = 0.0;

@@ -24,10 +24,9 @@
 // outputs are requested; otherwise the one-wave kernel, whose sector-window
 // tail handles any alignment.  The last, partial workgroup stores each
 // chunk through the slow tail.  Gradient atomics (gradient_mode 2) as the
-// one-wave kernel.  Two more forms are built only on request, each measured
-// slower than the one-wave kernel it would replace: the
-// fused gradient's points form (kGradF, -DCSE_GROUP_STORE_FP=1) and the
-// CompressedRowSparseMatrix form (kCrs, -DCSE_GROUP_STORE_CRS=1).
+// one-wave kernel.  The CompressedRowSparseMatrix form (kCrs) is built only
+// on request (-DCSE_GROUP_STORE_CRS=1): measured slower than the one-wave
+// CRS kernel, as was a fused-gradient form (removed).
 #ifndef CSE_GROUP_STORE_KERNEL_HPP_
 #define CSE_GROUP_STORE_KERNEL_HPP_
 
@@ -74,24 +73,12 @@ struct QuadPart {
   static constexpr int n(int r) { return (hi < re(r) ? hi : re(r)) - s(r) > 0 ? (hi < re(r) ? hi : re(r)) - s(r) : 0; }
 };
 
-// The fused gradient's per-wave stores (gradient_mode 0, points only): the
-// point rows that are this wave's alone and the two boundary entries
-// (FusedGrad), exec-masked, after the wave's runs.  Passed as values: a
-// struct handed down by pointer stayed in scratch (96 B a lane).
-struct GroupGradStores {
-  double* gp;
-  double* sp;
-  double g0, g1, g2;
-  cse_v4i sq0, sq1;
-  bool interior, writer;
-};
-
 // Read wave w's pieces from the workgroup image and store them, region by
 // region (at most three runs).
-template <int kW, int kSched, int w, bool kG, int kFk, int kEk, int kVm>
+template <int kW, int kSched, int w, int kFk, int kEk, int kVm>
 __device__ __forceinline__ void QuadTail(const double* img, double* const bases[3], int lane,
                                          double* v_partial, double v_wsum, bool failed,
-                                         int* status_dst, GroupGradStores gs) {
+                                         int* status_dst) {
   using P = QuadPart<kW, kSched, w, kFk, kEk>;
   constexpr int N = P::N;
   static_assert(N > 0 && N <= 24, "pieces per wave");
@@ -118,37 +105,24 @@ __device__ __forceinline__ void QuadTail(const double* img, double* const bases[
     QuadRun<P::n(1), P::n(0)>(b1, q);
     QuadRun<P::n(2), P::n(0) + P::n(1)>(b2, q);
   }
-  if constexpr (kG) {
-    if (gs.interior) {
-      StoreB64At<0>(gs.gp, gs.g0);
-      StoreB64At<8>(gs.gp, gs.g1);
-      StoreB64At<16>(gs.gp, gs.g2);
-    }
-    if (gs.writer) {
-      StoreNt16<0, 1>(gs.sp, gs.sq0);
-      StoreNt16<16, 1>(gs.sp, gs.sq1);
-    }
-  }
   if (lane == 0) {
     StoreB64(v_partial, v_wsum);
     if (failed) StoreB32(status_dst, 1);
   }
   KeepAlive<N>(q);
-  if constexpr (kG) asm volatile("" ::"v"(gs.gp), "v"(gs.sp), "v"(gs.g0), "v"(gs.g1), "v"(gs.g2), "v"(gs.sq0), "v"(gs.sq1));
   asm volatile("" ::"v"(b0), "v"(b1), "v"(b2), "v"(v_partial), "v"(v_wsum));
 }
 
-template <int kW, int kSched, bool kG = false, int kFk = kQuadFk, int kEk = kQuadEk, int kVm = 0, int w = 0>
+template <int kW, int kSched, int kFk = kQuadFk, int kEk = kQuadEk, int kVm = 0, int w = 0>
 __device__ __forceinline__ void QuadTailFor(int wave, const double* img, double* const bases[3], int lane,
                                             double* v_partial, double v_wsum, bool failed,
-                                            int* status_dst, GroupGradStores gs = {}) {
+                                            int* status_dst) {
   if constexpr (w < kW) {
     if (wave == w) {
-      QuadTail<kW, kSched, w, kG, kFk, kEk, kVm>(img, bases, lane, v_partial, v_wsum, failed, status_dst, gs);
+      QuadTail<kW, kSched, w, kFk, kEk, kVm>(img, bases, lane, v_partial, v_wsum, failed, status_dst);
       return;
     }
-    QuadTailFor<kW, kSched, kG, kFk, kEk, kVm, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst,
-                                                 gs);
+    QuadTailFor<kW, kSched, kFk, kEk, kVm, w + 1>(wave, img, bases, lane, v_partial, v_wsum, failed, status_dst);
   }
 }
 
@@ -156,23 +130,18 @@ __device__ __forceinline__ void QuadTailFor(int wave, const double* img, double*
 template <int kW, int kPadKiB>
 constexpr int kQuadWavesPerEu = ((160 / (13 * kW + kPadKiB)) * kW + 3) / 4;
 
-// kGradF: the fused gradient's points-only form (gradient_mode 0; the
-// slot-0 rows come from CameraGradientKernel), as
-// EvaluateAffineChunksFusedPointsW1.
 // kCrs: CompressedRowSparseMatrix values (block_jacobian_writer's CRS
 // sibling, compressed_row_jacobian_writer.cc): a block's NR rows of N = 12
 // columns are contiguous, so a workgroup's four chunks own one 48 KiB run of
 // rows and one 4 KiB run of residuals; each lane stages its rows with the
 // group's column offsets (camera and point columns in either order).
-template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kGradF = false, bool kCrs = false,
-          int kVm = 0>
+template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kCrs = false, int kVm = 0>
 __global__ __launch_bounds__(kW * kWave) __attribute__((amdgpu_waves_per_eu(kQuadWavesPerEu<kW, kPadKiB>))) void
 EvaluateAffineChunksGroupStore(const GroupArgs a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   constexpr int N = S0 + S1;
   static_assert(NR == 2 && S0 == 9 && S1 == 3, "Snavely-shaped kinds");
-  static_assert(!(kCrs && kGradF), "the fused gradient is a BlockSparseMatrix form");
   // KiB per chunk of the Jacobian regions: BSM F 9 and E 3, CRS rows 12
   constexpr int kFk = kCrs ? kQuadFk + kQuadEk : kQuadFk, kEk = kCrs ? 0 : kQuadEk;
   constexpr int kImg = (13 * kW + kPadKiB) * 128;  // doubles
@@ -194,7 +163,6 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok = true;
   double cost = 0.0;
-  int id1 = 0;
   if (has) {
     AffineInputs<K> in;
     const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
@@ -204,34 +172,14 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
     if (ok && a.check_finite)
       ok = !(AnyNonFinite<NR>(r) || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1));
     cost = LossAndCorrect<K, kLoss, true>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
-    if (!kGradF && a.gradient != nullptr && active) {  // gradient_mode 2: FP64 atomics, as the reference
+    if (a.gradient != nullptr && active) {  // gradient_mode 2: FP64 atomics, as the reference
       AddGradientSlot<NR, S0>(a.gradient + a.delta_base[0] + (int64_t)S0 * in.id0, S0, r, J0);
       AddGradientSlot<NR, S1p>(a.gradient + a.delta_base[1] + (int64_t)S1 * in.id1, S1, r, J1);
     }
-    id1 = in.id1;
   }
   const double wsum = WaveSumLane0(active ? cost : 0.0);
   const bool failed = __ballot(active && !ok) != 0;
   double* v_partial = a.partials + c;
-  // The fused gradient's slot-1 (point) rows: per wave, as the one-wave
-  // points kernel (FusedGrad; exec-masked stores after the runs).
-  FusedGrad<K> fg;
-  GroupGradStores gs{};
-  if constexpr (kGradF) {
-    if (has) {
-      fg.Compute(r, J0, J1, id1, active, lane, nw, c);
-      gs.interior = fg.interior;
-      gs.writer = fg.writer;
-      gs.gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
-      gs.sp = a.gside + 4 * fg.entry;
-      gs.g0 = fg.g1[0];
-      gs.g1 = fg.g1[1];
-      gs.g2 = fg.g1[2];
-      gs.sq0 = AsV4i(fg.g1[0], fg.g1[1]);
-      gs.sq1 = AsV4i(fg.g1[2], fg.g1[3]);
-    }
-  }
-
   const int64_t wg0 = (int64_t)blockIdx.x * kW * kWave;  // the workgroup's first block
   // CRS: the first row's offset (the slots' first columns, either order)
   const int64_t row0 = a.jac_base[0][0] < a.jac_base[1][0] ? a.jac_base[0][0] : a.jac_base[1][0];
@@ -267,32 +215,13 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
     *reinterpret_cast<double2*>(rw + lane * NR) = make_double2(r[0], r[1]);
     __syncthreads();
     double* const bases[3] = {fbase, ebase, rbase};
-    QuadTailFor<kW, kSched, kGradF, kFk, kEk, kVm>(w, img, bases, lane, v_partial, wsum, failed, a.status, gs);
+    QuadTailFor<kW, kSched, kFk, kEk, kVm>(w, img, bases, lane, v_partial, wsum, failed, a.status);
     return;
   }
   // The last (partial) workgroup or unaligned outputs: each wave its own
   // chunk through the slow tail, in its own F region (CRS: its 12 KiB of rows).
   __syncthreads();  // every wave's gather landing area is free again
   if (has) StageAndStore<K, true, kCrs>(a, fw, lane, active, i0, nw, r, J0, J1);
-  if constexpr (kGradF) {
-    if (has) {  // plain stores, as AffineChunkBody's slow tail
-      if (fg.interior) {
-        double* g = a.gfused + a.delta_base[1] + 3LL * fg.key;
-        g[0] = fg.g1[0];
-        g[1] = fg.g1[1];
-        g[2] = fg.g1[2];
-      }
-      if (fg.writer) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a.gside[4 * fg.entry + q] = fg.g1[q];
-      }
-      if (nw == 1 && lane == 0) {  // a one-block wave: its zero entry
-        double* e = a.gside + 4 * (2 * c + 1);
-        e[0] = e[1] = e[2] = 0.0;
-        e[3] = fg.g1[3];
-      }
-    }
-  }
   if (lane == 0 && has) {  // slots past the last chunk stay 0 (zeroed at cse_create)
     *v_partial = wsum;
     if (failed) *a.status = 1;
