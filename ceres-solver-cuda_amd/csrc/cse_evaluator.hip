@@ -937,6 +937,9 @@ int Validate(const cse_problem_desc* d) {
 #ifndef CSE_GRAD_ASSIGN
 #define CSE_GRAD_ASSIGN 1
 #endif
+#ifndef CSE_GRAD_TAIL_MERGED
+#define CSE_GRAD_TAIL_MERGED 1
+#endif
 int CamGradPasses(const cse_residual_group& g, const KindShape& k) {
   int32_t lo = INT32_MAX, hi = INT32_MIN;
   for (int64_t i = 0; i < g.num_blocks; ++i) {
@@ -1463,17 +1466,12 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
 
 // After the points kernel and CameraGradientKernel: the slot-1 boundary
 // entries, then the slot-0 rows from the chunk sums, in a fixed order.
-// assign (grad_exact): the rows are written, not added to.
+// assign (grad_exact): the rows are written, not added to.  The boundary
+// entries and the camera rows in one launch (GradientTailKernel).
 int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s, bool assign = false) {
   const Group::GradPlan& P = G.grad[0];
   const int64_t entries = 2 * ((G.n + cse::kWave - 1) / cse::kWave);
-  const dim3 bgrid((unsigned)((entries + cse::kBlockThreads - 1) / cse::kBlockThreads));
-  if (assign)
-    hipLaunchKernelGGL((cse::GradientBoundaryKernel<3, true>), bgrid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
-                       entries, out, G.delta_base[1]);
-  else
-    hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>), bgrid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
-                       entries, out, G.delta_base[1]);
+  const int64_t bwg = (entries + cse::kBlockThreads - 1) / cse::kBlockThreads;
   cse::GradArgs ga{};
   ga.count = P.count;
   ga.lo = P.lo;
@@ -1481,11 +1479,29 @@ int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s, bool assign = f
   ga.delta_base = G.delta_base[0];
   ga.delta_tab = G.const0 ? G.delta0.p + (P.lo - G.slot0_lo) : nullptr;
   const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
-  const dim3 cgrid((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads));
+  const int64_t cwg = (ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads;
+  if (CSE_GRAD_TAIL_MERGED == 0) {  // two launches (A/B)
+    if (assign) {
+      hipLaunchKernelGGL((cse::GradientBoundaryKernel<3, true>), dim3((unsigned)bwg), dim3(cse::kBlockThreads), 0,
+                         s, G.gside.p, entries, out, G.delta_base[1]);
+      hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9, true>), dim3((unsigned)cwg), dim3(cse::kBlockThreads),
+                         0, s, ga, ch);
+    } else {
+      hipLaunchKernelGGL((cse::GradientBoundaryKernel<3>), dim3((unsigned)bwg), dim3(cse::kBlockThreads), 0, s,
+                         G.gside.p, entries, out, G.delta_base[1]);
+      hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), dim3((unsigned)cwg), dim3(cse::kBlockThreads), 0, s,
+                         ga, ch);
+    }
+    CSE_HIP(hipGetLastError());
+    return CSE_OK;
+  }
+  const dim3 grid((unsigned)(bwg + cwg));
   if (assign)
-    hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9, true>), cgrid, dim3(cse::kBlockThreads), 0, s, ga, ch);
+    hipLaunchKernelGGL((cse::GradientTailKernel<3, 9, true>), grid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
+                       entries, G.delta_base[1], bwg, ga, ch);
   else
-    hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), cgrid, dim3(cse::kBlockThreads), 0, s, ga, ch);
+    hipLaunchKernelGGL((cse::GradientTailKernel<3, 9, false>), grid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
+                       entries, G.delta_base[1], bwg, ga, ch);
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }

@@ -136,10 +136,8 @@ __global__ __launch_bounds__(kBlockThreads) void GradientLanesKernel(const GradA
 
 // kAssign: the row is written, not added to (the evaluator's grad_exact:
 // every row of the gradient is written once and it is not zeroed first).
-template <int S, bool kAssign = false>
-__global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const GradArgs g,
-                                                                           const GradChunks ch) {
-  const int64_t p = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+template <int S, bool kAssign>
+__device__ __forceinline__ void ChunkReduceRow(const GradArgs& g, const GradChunks& ch, int64_t p) {
   if (p >= g.count) return;
   // A block without chunks adds nothing (and a constant one has no row).
   if (!kAssign && ch.chunk_off[p] == ch.chunk_off[p + 1]) return;
@@ -157,6 +155,12 @@ __global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const
     else
       dst[c] += acc[c];
   }
+}
+
+template <int S, bool kAssign = false>
+__global__ __launch_bounds__(kBlockThreads) void GradientChunkReduceKernel(const GradArgs g,
+                                                                           const GradChunks ch) {
+  ChunkReduceRow<S, kAssign>(g, ch, (int64_t)blockIdx.x * kBlockThreads + threadIdx.x);
 }
 
 // Fused-gradient slot 0 (FusedGrad): each chunk of a parameter block's
@@ -203,13 +207,10 @@ __global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const dou
 // wave order, so their ids are non-decreasing; the first entry of each id
 // adds that id's entries in order and adds the sum to the row (no interior
 // run of any wave touched these rows).
-template <int S, bool kAssign = false>
-__global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const double* side,
-                                                                        int64_t count,
-                                                                        double* grad,
-                                                                        int64_t delta_base) {
+template <int S, bool kAssign>
+__device__ __forceinline__ void BoundaryEntry(const double* side, int64_t count, double* grad,
+                                              int64_t delta_base, int64_t e) {
   static_assert(S <= 3, "entries hold 3 sums and the id");
-  const int64_t e = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
   if (e >= count) return;
   // The entry, its predecessor's id and the next two entries in one round
   // trip (independent 16-byte loads; a key's entries are one to three in
@@ -260,6 +261,29 @@ __global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const do
     else
       dst[c] += acc[c];
   }
+}
+
+template <int S, bool kAssign = false>
+__global__ __launch_bounds__(kBlockThreads) void GradientBoundaryKernel(const double* side,
+                                                                        int64_t count,
+                                                                        double* grad,
+                                                                        int64_t delta_base) {
+  BoundaryEntry<S, kAssign>(side, count, grad, delta_base, (int64_t)blockIdx.x * kBlockThreads + threadIdx.x);
+}
+
+// Gradient mode 0's tail in one launch: workgroups [0, boundary_wg) add the
+// slot-1 boundary entries (GradientBoundaryKernel), the rest the slot-0
+// chunk partials per camera (GradientChunkReduceKernel).  The two touch
+// disjoint rows.
+template <int S1, int S0, bool kAssign>
+__global__ __launch_bounds__(kBlockThreads) void GradientTailKernel(const double* side, int64_t entries,
+                                                                    int64_t delta_base1, int64_t boundary_wg,
+                                                                    const GradArgs g, const GradChunks ch) {
+  const int64_t b = blockIdx.x;
+  if (b < boundary_wg)
+    BoundaryEntry<S1, kAssign>(side, entries, g.grad, delta_base1, b * kBlockThreads + threadIdx.x);
+  else
+    ChunkReduceRow<S0, kAssign>(g, ch, (b - boundary_wg) * kBlockThreads + threadIdx.x);
 }
 
 // Identity order (the points of a Schur-ordered problem): one 64-thread
