@@ -204,6 +204,8 @@ struct Group {
     DevBuf<int64_t> chunk_begin, chunk_off;
     DevBuf<int32_t> chunk_pb;  // parameter block (id) of each chunk
     DevBuf<int32_t> chunk_order;  // passes > 1: the chunks pass-major (BuildGradPlan)
+    DevBuf<int32_t> xcd_order;    // CSE_CAMGRAD_XCD: CameraGradientKernel's slots (-1: none)
+    int64_t nslots = 0;
     int passes = 1;
     DevBuf<double> chunk_partial;
     int64_t nchunks = 0;
@@ -928,6 +930,11 @@ int Validate(const cse_problem_desc* d) {
 #ifndef CSE_CAMGRAD_PASS_MB
 #define CSE_CAMGRAD_PASS_MB 96
 #endif
+// CSE_CAMGRAD_XCD 1 (A/B): CameraGradientKernel's passes 8 times finer and
+// dealt to the XCDs (BuildGradPlan's xcd_order).
+#ifndef CSE_CAMGRAD_XCD
+#define CSE_CAMGRAD_XCD 0
+#endif
 // The camera sums over written contributions (gradient_mode 3, the Schur
 // and CGNR operators' F^T u) take the same plan's chunks pass-major too
 // (GradientContribKernel's order; 0: chunk order, camera-major).
@@ -950,6 +957,7 @@ int CamGradPasses(const cse_residual_group& g, const KindShape& k) {
   const double bytes = 8.0 * k.s1 * ((double)hi - lo + 1) + (8.0 * k.data + 4.0) * g.num_blocks;
   const double per = (double)CSE_CAMGRAD_PASS_MB * 1e6;
   const int p = (int)std::ceil(bytes / per);
+  if (CSE_CAMGRAD_XCD != 0) return std::max(1, std::min(512, 8 * p));
   return std::max(1, std::min(64, p));
 }
 
@@ -1036,6 +1044,27 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
         for (int64_t c = 0; c < plan->nchunks; ++c)
           if (cpass[c] == t) order.push_back((int32_t)c);
       if ((rc = plan->chunk_order.upload(order.data(), order.size(), s))) return rc;
+      if (CSE_CAMGRAD_XCD != 0 && j == 0) {
+        // XCD x (workgroups b with b % 8 == x under round-robin placement)
+        // takes the passes t with t % 8 == x, pass-major: the eight XCDs
+        // gather from eight different point ranges, each small enough for
+        // its own L2.  Workgroup 8 i + x holds list x's chunks [W i, W i + W).
+        constexpr int W = cse::kWavesPerBlock;
+        std::vector<std::vector<int32_t>> lx(8);
+        for (int32_t c : order) lx[cpass[c] % 8].push_back(c);
+        size_t longest = 0;
+        for (auto& l : lx) longest = std::max(longest, l.size());
+        const size_t rows = (longest + W - 1) / W;
+        std::vector<int32_t> xo(rows * 8 * W, -1);
+        for (size_t i = 0; i < rows; ++i)
+          for (int x = 0; x < 8; ++x)
+            for (int k = 0; k < W; ++k) {
+              const size_t idx = i * W + k;
+              if (idx < lx[x].size()) xo[(i * 8 + x) * W + k] = lx[x][idx];
+            }
+        plan->nslots = (int64_t)xo.size();
+        if ((rc = plan->xcd_order.upload(xo.data(), xo.size(), s))) return rc;
+      }
     }
     // Chunk c covers [begin[c], begin[c + 1]): a parameter block's last
     // chunk ends at off[p + 1], where the next non-empty one starts.
@@ -1421,9 +1450,10 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
   cg.sid1 = G.sid1.p;
   cg.chunk_pb = P.chunk_pb.p;
   cg.chunk_begin = P.chunk_begin.p;
-  cg.chunk_order = P.chunk_order.p;
+  cg.chunk_order = P.xcd_order.p ? P.xcd_order.p : P.chunk_order.p;
   cg.partial = P.chunk_partial.p;
   cg.nchunks = P.nchunks;
+  cg.nslots = P.xcd_order.p ? P.nslots : P.nchunks;
   cg.loss.a = G.loss.a;
   cg.loss.scale = G.loss.scale;
   cg.loss.scaled = G.loss.scaled;
@@ -1438,7 +1468,8 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
     cg.ppad_lo = G.grad[1].lo;
   }
   constexpr int W = kCamGradWavesPerWg;
-  const dim3 grid((unsigned)((P.nchunks + W - 1) / W));
+  static_assert(CSE_CAMGRAD_XCD == 0 || W == cse::kWavesPerBlock, "xcd_order assumes 4-wave workgroups");
+  const dim3 grid((unsigned)((cg.nslots + W - 1) / W));
   if (P.nchunks > 0) {
     auto launch = [&](auto kd) {
       using K = decltype(kd);
@@ -1456,7 +1487,7 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
                              dim3(W * cse::kWave), 0, s, cg);
       }
     };
-    if (G.jet) cse::LaunchJetCameraGradient(G.loss.kind, cg, P.nchunks, s);
+    if (G.jet) cse::LaunchJetCameraGradient(G.loss.kind, cg, cg.nslots, s);
     else if (G.kind == kKindQuaternionTangent) launch(cse::SnavelyQuaternionTangentKind{});
     else launch(cse::SnavelyKind{});
   }

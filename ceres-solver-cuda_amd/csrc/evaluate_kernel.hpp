@@ -1638,6 +1638,7 @@ struct CamGradArgs {
   const int32_t* chunk_order;  // [nchunks] the order to take them in (null: 0, 1, ...)
   double* partial;             // [nchunks][S0]
   int64_t nchunks;
+  int64_t nslots;              // waves launched; chunk_order[slot] < 0: none
   LossParams loss;
   int apply_loss;
   // Groups with constant slot-0 blocks: the camera from the repacked table
@@ -1709,10 +1710,11 @@ CameraGradientKernel(const CamGradArgs g) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = kWPB == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t slot = (int64_t)blockIdx.x * kWPB + wave;
-  if (slot >= g.nchunks) return;
+  if (slot >= g.nslots) return;
   // Pass-major (BuildGradPlan): the resident waves gather from one point
   // range at a time, small enough to stay in the Infinity Cache.
   const int64_t cid = g.chunk_order ? (int64_t)g.chunk_order[slot] : slot;
+  if (cid < 0) return;
   const int64_t q0 = g.chunk_begin[cid], q1 = g.chunk_begin[cid + 1];
   constexpr int X0 = Tr::X0;
   const double* cam = g.packed0 ? g.packed0 + (int64_t)g.packed_stride * (g.chunk_pb[cid] - g.packed_lo)

@@ -24,7 +24,7 @@ JetLaunchFn JetSnavelyFusedPoints(int loss, bool crs);
 JetLaunchFn JetSnavelyTable(int loss);
 // CameraGradientKernel with the camera partials by Jet<9>, kWPB waves per
 // workgroup, one chunk per wave.
-void LaunchJetCameraGradient(int loss, const CamGradArgs& g, int64_t nchunks, hipStream_t s);
+void LaunchJetCameraGradient(int loss, const CamGradArgs& g, int64_t nslots, hipStream_t s);
 
 }  // namespace cse
 

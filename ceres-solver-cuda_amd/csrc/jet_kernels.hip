@@ -64,9 +64,9 @@ JetLaunchFn JetSnavelyTable(int loss) {
   }
 }
 
-void LaunchJetCameraGradient(int loss, const CamGradArgs& g, int64_t nchunks, hipStream_t s) {
+void LaunchJetCameraGradient(int loss, const CamGradArgs& g, int64_t nslots, hipStream_t s) {
   constexpr int W = kWavesPerBlock;
-  const dim3 grid((unsigned)((nchunks + W - 1) / W));
+  const dim3 grid((unsigned)((nslots + W - 1) / W));
   switch (loss) {
     case kLossHuber:
       hipLaunchKernelGGL((CameraGradientKernel<K, kLossHuber, W>), grid, dim3(W * kWave), 0, s, g);
