@@ -14,10 +14,11 @@
 // short segments (9, 3 and 1 KiB) per wave.
 //
 // Measured (same-process interleaved A/Bs against the
-// one-wave-workgroup kernel, bit-identical outputs): -1.6 %, -1.4 %, -2.3 %
-// on three boxes (profiles/round5/r5a, r5b, r5c).  Other shapes of the
+// one-wave-workgroup kernel, bit-identical outputs): -1.4 % to -2.4 % on
+// six boxes (profiles/round5/r5a-r5d, r5f, r5g).  Other shapes of the
 // tuning build (kW = 2, 3, 5, 6, 8; 8 waves per CU; waves 0-2 taking F in
-// thirds and wave 3 E and R, kSched 1) were slower.
+// thirds and wave 3 E and R, kSched 1; two LDS phases; a persistent
+// pipelined form; stores in flight capped per wave, kVm) were slower.
 //
 // Used when the group's residual, E and F bases are 64-byte aligned (then
 // every workgroup's runs are: 9216, 3072 and 1024 bytes per chunk) and both
