@@ -73,7 +73,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=25)
     ap.add_argument("--config", default="problem-13682-4456117", choices=list(bal.CONFIGS))
     ap.add_argument("--loss", default="huber", choices=["trivial", "huber", "cauchy"])
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
