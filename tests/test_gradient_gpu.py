@@ -115,3 +115,57 @@ def test_fused_gradient_needs_exclusive_points(gpu):
     if shared:
         assert info.num_fused_gradient_groups == 0
     assert_parity(got, ref, "two groups")
+
+
+def _device_gradient(prog, fill=np.nan):
+    """residuals + gradient + Jacobian through the device entry point, the
+    gradient buffer filled with `fill` first (gradient_mode 0)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, device=0)
+    try:
+        state = torch.from_numpy(prog.state).to(dev)
+        cost = torch.zeros(1, dtype=torch.float64, device=dev)
+        res = torch.empty(prog.num_residuals, dtype=torch.float64, device=dev)
+        grad = torch.full((prog.num_effective_parameters,), fill, dtype=torch.float64, device=dev)
+        jac = torch.empty(prog.num_jacobian_values, dtype=torch.float64, device=dev)
+        torch.cuda.synchronize()
+        ev.evaluate_device(state.data_ptr(), cost.data_ptr(), res.data_ptr(), grad.data_ptr(),
+                           jac.data_ptr())
+        assert ev.wait() == 0
+        return (True, float(cost.item()), res.cpu().numpy(), grad.cpu().numpy(),
+                jac.cpu().numpy()), ev.info()
+    finally:
+        ev.close()
+
+
+def test_gradient_rows_written_once_into_a_dirty_buffer(gpu):
+    """Every camera and point observed (Group::grad_exact): the fused
+    gradient writes each row exactly once and the buffer is not zeroed
+    first (CSE_GRAD_ASSIGN) -- a NaN-filled buffer comes back complete."""
+    prog = bal.synthetic_program((24, 3000, 20000), loss=ca.Loss.huber(1.0), seed=11)
+    assert len(np.unique(prog.groups[0].ids[:, 0])) == 24
+    got, info = _device_gradient(prog)
+    assert info.num_fused_gradient_groups == 1
+    assert_parity(got, oracle_eval(prog), "assigned rows")
+
+
+@pytest.mark.parametrize("drop_cams,drop_pts", [((7,), (100,)), ((23,), ()), ((0,), (0, 2999))])
+def test_gradient_with_unobserved_parameter_blocks(gpu, drop_cams, drop_pts):
+    """Cameras or points that no residual block uses (inside the id ranges
+    or at their ends): their gradient rows are zero, so the buffer is zeroed
+    first (grad_exact false) and the rest added -- a NaN-filled buffer comes
+    back equal to the oracle."""
+    cams, pts, ci, pi, obs = bal.synthetic(24, 3000, 20000, seed=5)
+    keep = ~np.isin(ci, drop_cams) & ~np.isin(pi, drop_pts)
+    prog = bal.program(cams, pts, ci[keep], pi[keep], obs[keep], loss=ca.Loss.huber(1.0))
+    got, info = _device_gradient(prog)
+    ref = oracle_eval(prog)
+    assert_parity(got, ref, ("unobserved", drop_cams, drop_pts))
+    P = pts.shape[0]
+    g = got[3]
+    for p in drop_pts:
+        assert np.all(g[3 * p:3 * p + 3] == 0.0)
+    cam0 = 3 * P
+    for c in drop_cams:
+        assert np.all(g[cam0 + 9 * c:cam0 + 9 * c + 9] == 0.0)
