@@ -438,11 +438,11 @@ void LaunchTwoRoundProbe(const cse::GroupArgs& a0, int64_t num_wg, hipStream_t s
 
 // Tuning build: kW-wave workgroups storing their kW chunks' outputs as long
 // runs (group_store_kernel.hpp; the product launches kW = 4).  Variants 90-98.
-template <class K, int L, int kW, int kSched, int kPad = 0, int kVm = 0>
+template <class K, int L, int kW, int kSched, int kPad = 0, int kVm = 0, int kPrio = 0>
 void LaunchQuad(const cse::GroupArgs& a, int64_t num_wg, hipStream_t s) {
   (void)num_wg;
   const int64_t chunks = (a.n + cse::kWave - 1) / cse::kWave;
-  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad, false, kVm>), dim3((unsigned)((chunks + kW - 1) / kW)),
+  hipLaunchKernelGGL((cse::EvaluateAffineChunksGroupStore<K, L, kW, kSched, kPad, false, kVm, kPrio>), dim3((unsigned)((chunks + kW - 1) / kW)),
                      dim3(kW * cse::kWave), 0, s, a);
 }
 
@@ -713,6 +713,10 @@ LaunchFn TuningVariant(int v, bool jac) {
     case 101: return &LaunchQuad<K, L, 4, 0, 0, 2>;
     case 102: return &LaunchQuad<K, L, 4, 0, 0, 4>;
     case 103: return &LaunchQuad<K, L, 4, 0, 0, 8>;
+    // the group-store kernel at s_setprio 1 / 2 / 3 until its store tail
+    case 104: return &LaunchQuad<K, L, 4, 0, 0, 0, 1>;
+    case 105: return &LaunchQuad<K, L, 4, 0, 0, 0, 2>;
+    case 106: return &LaunchQuad<K, L, 4, 0, 0, 0, 3>;
     default: return nullptr;
   }
 }

@@ -136,7 +136,9 @@ constexpr int kQuadWavesPerEu = ((160 / (13 * kW + kPadKiB)) * kW + 3) / 4;
 // columns are contiguous, so a workgroup's four chunks own one 48 KiB run of
 // rows and one 4 KiB run of residuals; each lane stages its rows with the
 // group's column offsets (camera and point columns in either order).
-template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kCrs = false, int kVm = 0>
+// kPrio (tuning): the wave at s_setprio kPrio from its start to its store
+// tail, so that waves still loading issue ahead of waves storing.
+template <class K, int kLoss, int kW, int kSched, int kPadKiB, bool kCrs = false, int kVm = 0, int kPrio = 0>
 __global__ __launch_bounds__(kW * kWave) __attribute__((amdgpu_waves_per_eu(kQuadWavesPerEu<kW, kPadKiB>))) void
 EvaluateAffineChunksGroupStore(const GroupArgs a) {
   using Tr = KindTraits<K>;
@@ -164,6 +166,7 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
   double r[NR], J0[NR * S0], J1[NR * S1p];
   bool ok = true;
   double cost = 0.0;
+  if constexpr (kPrio > 0) __builtin_amdgcn_s_setprio(kPrio);
   if (has) {
     AffineInputs<K> in;
     const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
@@ -214,6 +217,7 @@ EvaluateAffineChunksGroupStore(const GroupArgs a) {
         *reinterpret_cast<double2*>(ew + lane * NR * S1 + q) = make_double2(J1[q], J1[q + 1]);
     }
     *reinterpret_cast<double2*>(rw + lane * NR) = make_double2(r[0], r[1]);
+    if constexpr (kPrio > 0) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     double* const bases[3] = {fbase, ebase, rbase};
     QuadTailFor<kW, kSched, kFk, kEk, kVm>(w, img, bases, lane, v_partial, wsum, failed, a.status);
