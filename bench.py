@@ -33,6 +33,11 @@ same run (each with its own barrier-bracketed timing, max over ranks):
   residual_only  residuals + cost (trust_region_minimizer.cc:770-788)
   jet            the headline evaluation with the Jacobian by Jet<double, 12>
                  (cse_options.jacobian_form; the headline uses the closed form)
+  user_functor   the same workload with a *user* functor, BundlerResidual
+                 (bundle_adjustment_test_util.h:188-227), compiled in a user
+                 TU against ceres_amd/autodiff_cuda.h
+                 (examples/build/libuser_functors.so) and registered through
+                 cse_register_functor: the reference's usage model
   host_strips    evaluation + D2H of each rank's residual and Jacobian
                  strips into pinned host memory (the reference's seam,
                  README.md:198-200; PCIe-inclusive, never `value`)
@@ -105,6 +110,9 @@ def parse():
     ap.add_argument("--secondary-steps", type=int, default=20)
     ap.add_argument("--host-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="BASELINE.json configs[0]: problem-16 on the CPU ProgramEvaluator "
+                         "restatement at num_threads=1 (no GPU); prints its own JSON line")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the CPU baseline's all-core leg; 0 = one per physical core "
                          "of the affinity mask (legs at the box's CPU share -- the cgroup quota, "
@@ -223,6 +231,29 @@ def _oracle_module():
     return O, build
 
 
+def user_functor_kind(name):
+    """A kind of the example user functor library (examples/user_functors.hip),
+    loaded into this process's libcse.so."""
+    import ctypes
+    lib = ca.load_functor_library(os.path.join(REPO, "examples", "build", "libuser_functors.so"))
+    lib.cse_example_kind_name.restype = ctypes.c_char_p
+    kinds = (ctypes.c_int32 * 64)()
+    n = lib.cse_example_register(kinds, 64)
+    if n < 0:
+        raise RuntimeError("cse_example_register: " + ca._cse.last_error())
+    names = [lib.cse_example_kind_name(i).decode() for i in range(n)]
+    return kinds[names.index(name)]
+
+
+def group_store_eligible(res_ptr, jac_ptr, nblocks):
+    """The library's choice of the Snavely BlockSparse residual+Jacobian
+    kernel for a shard-local evaluator (GroupStoreEligible,
+    csrc/group_store_kernel.hpp): residuals, E cells (at 0) and F cells (at
+    6 n doubles) on 64-byte boundaries -> EvaluateAffineChunksGroupStore,
+    else the one-wave EvaluateAffineChunksTwoRoundW1."""
+    return (res_ptr % 64 == 0 and jac_ptr % 64 == 0 and (jac_ptr + 48 * nblocks) % 64 == 0)
+
+
 def cpu_baseline(args, arrays, threads, share):
     """The oracle on bounded, point-bucket-aligned samples of the workload:
     residual+Jacobian and residual-only at `threads` (one per physical core
@@ -289,12 +320,62 @@ def cpu_baseline(args, arrays, threads, share):
                        f"fastest Jacobian leg ({best['threads']} threads), blocks/s / {total:,}; "
                        f"cores = the CPUs that leg could use (cgroup quota "
                        f"{quota if quota is not None else 'none'})"),
-            "build": build, "host": host, "legs": legs}
+            "build": build, "host": host, "legs": legs,
+            "configs0": configs0(O, build, args.seed)}
+
+
+def configs0(O, build, seed, reps=10):
+    """BASELINE.json configs[0]: problem-16-22106 (16 cameras, 22,106 points,
+    83,718 SnavelyReprojectionError<2,9,3> blocks), no loss, BlockSparseMatrix,
+    the CPU ProgramEvaluator restated (oracle/) at num_threads = 1 -- the
+    reference's plumbing configuration, no GPU.  Residual+Jacobian and
+    residual-only, median of `reps` after a warm-up, as the reference's
+    evaluation benchmark times them (evaluation_benchmark.cc:203-266)."""
+    prog = bal.synthetic_program("problem-16-22106", seed=seed)
+    ev = O.OracleProgram.from_program(prog).evaluator(1)
+    out = {}
+    for jac in (True, False):
+        r = np.empty(prog.num_residuals)
+        j = np.empty(prog.num_jacobian_values) if jac else None
+        ev.run(prog.state, None, r, None, j)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ok, cost = ev.run(prog.state, None, r, None, j)
+            times.append(time.perf_counter() - t0)
+            assert ok
+        t = float(np.median(times))
+        out["jacobian" if jac else "residual_only"] = {
+            "value": 1.0 / t, "unit": "evals/s", "median_s": t, "reps": reps, "cost": cost}
+    ev.close()
+    out.update({"workload": "problem-16-22106 SnavelyReprojectionError<2,9,3>, no loss, "
+                            "block_sparse, CPU ProgramEvaluator restatement (oracle/), "
+                            "num_threads=1 (BASELINE.json configs[0])",
+                "blocks": prog.num_residual_blocks, "threads": 1, "build": build})
+    return out
+
+
+def cpu_only(args):
+    """--cpu-only: BASELINE.json configs[0] alone, on this host's CPU (no GPU,
+    no torch): one JSON line."""
+    O, build = _oracle_module()
+    c0 = configs0(O, build, args.seed, reps=max(3, args.steps))
+    line = {"metric": "residual+Jacobian evaluations/sec on BAL problem-16 (CPU ProgramEvaluator, "
+                      "num_threads=1; BASELINE.json configs[0], not the headline)",
+            "value": c0["jacobian"]["value"], "unit": "evals/s", "n_gpus": 0,
+            "steps": c0["jacobian"]["reps"], "higher_is_better": True, "dtype": "f64",
+            "data": "synthetic (BAL-shaped: exact header counts, seeded generator)",
+            "config": {"workload": c0["workload"], "blocks": c0["blocks"]},
+            "residual_only": c0["residual_only"], "build": build, "host": _host_info()}
+    print(json.dumps(line), flush=True)
+    return line
 
 
 # ---------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.cpu_only:
+        return cpu_only(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -468,6 +549,9 @@ def main():
         return float(t.item())
 
     tot_bytes = reduce_sum(bytes_launch)
+    nblk = se.shard.blocks[1] - se.shard.blocks[0]
+    store_eligible = (args.format == "block_sparse" and args.mode == "jacobian" and
+                      group_store_eligible(se.residuals.data_ptr(), se.jacobian.data_ptr(), nblk))
     # Per GPU: the ranks' bytes / N over the slowest rank's kernel time.
     achieved = tot_bytes / world / (kernel_ms_max * 1e-3) / 1e9
     value = units * args.steps / elapsed
@@ -558,6 +642,42 @@ def main():
             finally:
                 se, ev = saved
                 jev.close()
+            # The same workload with a user functor (BundlerResidual through
+            # cse_register_functor, its kernels compiled in the example's
+            # TU): the Jet<double, 12> evaluation of the user's own code,
+            # the same kernel template as the library's Jet form.
+            import copy
+            import dataclasses
+            uprog = copy.copy(prog)
+            uname = {"trivial": "BundlerResidual/Trivial", "huber": "BundlerResidual/Huber"}.get(args.loss)
+            if uname is not None:
+                uprog.groups = [dataclasses.replace(g, kind=user_functor_kind(uname)) for g in prog.groups]
+                uev = ca.Evaluator(uprog, device=dev_index, profile=True, stream=stream.cuda_stream)
+                uinfo = uev.info()
+                saved = se, ev
+
+                class _UserLeg:
+                    def wait_exchange(self):
+                        pass
+
+                    def wait(self):
+                        return uev.wait()
+
+                se, ev = _UserLeg(), uev
+                try:
+                    leg("user_functor",
+                        lambda: uev.evaluate_device(st_.data_ptr(), cost_.data_ptr(), res_.data_ptr(),
+                                                    None, jac_.data_ptr()),
+                        uinfo.bytes_jacobian_eval, ks,
+                        f"the headline workload with a user functor: {uname} "
+                        "(bundle_adjustment_test_util.h:188-227) compiled in a user TU against "
+                        "ceres_amd/autodiff_cuda.h (examples/user_functors.hip), registered by "
+                        "cse_register_functor; residuals + Jacobian (Jet<double, 12>) + cost: "
+                        "EvaluateAffineChunksTwoRoundW1<UserKind<BundlerResidual, ...>, ...>")
+                    secondary["user_functor"]["affine"] = uinfo.num_affine_groups == 1
+                finally:
+                    se, ev = saved
+                    uev.close()
         if world == 1 and args.config == "problem-13682-4456117" and not variant:
             # BASELINE.json configs[2] (problem-1778, HuberLoss,
             # CompressedRowSparseMatrix) in the same driver-timed run: its own
@@ -690,7 +810,7 @@ def main():
                 "kernel_ms_avg": kernel_ms,
                 "kernel_ms_avg_max_rank": kernel_ms_max,
                 "kernel": f"cse::EvaluateAffineChunks"
-                          f"{'FusedPointsW1' if args.gradient else (('GroupStore' if not quat and not args.held_cameras else 'TwoRoundW1') if args.format == 'block_sparse' else 'TwoRoundCrsW1')}"
+                          f"{'FusedPointsW1' if args.gradient else (('GroupStore' if not quat and not args.held_cameras and store_eligible else 'TwoRoundW1') if args.format == 'block_sparse' else 'TwoRoundCrsW1')}"
                           f"<{'SnavelyQuaternionTangentKind' if quat else 'SnavelyKind'}, {args.loss}, {args.format}> (+ repack"
                           f"{', CameraGradientKernel and the gradient tail' if args.gradient else ''})",
                 "per": "GPU (bytes of all ranks / N over the slowest rank's kernel time)",

@@ -6,13 +6,14 @@ include/cse.h); this package builds Programs and calls it.  There is no
 CPU fallback anywhere in the package.
 """
 from . import _cse, bal
-from ._cse import (LOSS_CAUCHY, LOSS_HUBER, LOSS_TRIVIAL, POINT_DISPLACEMENT_3_3,
+from ._cse import (LOSS_CAUCHY, LOSS_HUBER, LOSS_TRIVIAL, LOSS_USER, POINT_DISPLACEMENT_3_3,
                    SNAVELY_2_9_3, SNAVELY_NO_DISTORTION_2_7_3, SNAVELY_QUATERNION_2_10_3,
-                   FUNCTOR_SHAPES)
+                   FUNCTOR_SHAPES, functor_shape, load_functor_library)
 from .problem import (BLOCK_SPARSE, COMPRESSED_ROW, Evaluator, Loss, Program, ProblemCUDA,
                       ResidualGroup, host_register, host_unregister)
 
 __all__ = ["bal", "Evaluator", "Loss", "Program", "ProblemCUDA", "ResidualGroup",
            "BLOCK_SPARSE", "COMPRESSED_ROW", "SNAVELY_2_9_3", "SNAVELY_NO_DISTORTION_2_7_3",
            "SNAVELY_QUATERNION_2_10_3", "POINT_DISPLACEMENT_3_3", "LOSS_TRIVIAL", "LOSS_HUBER",
-           "LOSS_CAUCHY", "FUNCTOR_SHAPES", "host_register", "host_unregister"]
+           "LOSS_CAUCHY", "LOSS_USER", "FUNCTOR_SHAPES", "functor_shape", "load_functor_library",
+           "host_register", "host_unregister"]

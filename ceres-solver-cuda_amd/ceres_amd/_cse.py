@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libcse.so"))
 
-CSE_ABI_VERSION = 3
+CSE_ABI_VERSION = 4
 
 # cse_options.jacobian_form (cse_jacobian_form)
 JACOBIAN_CLOSED_FORM = 0
@@ -65,6 +65,12 @@ SCHUR_SCHUR_JACOBI = 2
 LOSS_TRIVIAL = 0
 LOSS_HUBER = 1
 LOSS_CAUCHY = 2
+LOSS_USER = 3  # a user LossFunctionCUDA compiled into a user functor kind
+USER_LOSS_BYTES = 64
+
+# User functor kinds (cse_register_functor) are numbered from here.
+FUNCTOR_USER_FIRST = 1000
+MAX_PARAMETER_BLOCKS = 10
 
 # cse_manifold_kind (include/cse.h)
 MANIFOLD_MATRIX = 0
@@ -73,7 +79,7 @@ MANIFOLD_QUATERNION_EUCLIDEAN = 1
 
 class cse_loss(C.Structure):
     _fields_ = [("kind", C.c_int32), ("scaled", C.c_int32), ("a", C.c_double),
-                ("scale", C.c_double)]
+                ("scale", C.c_double), ("user", C.c_double * (USER_LOSS_BYTES // 8))]
 
 
 class cse_parameter_block(C.Structure):
@@ -171,6 +177,8 @@ SIGNATURES = {
     "cse_compressed_row_layout": (C.c_int, [C.c_int64, P_pb, C.c_int64, P_i64, P_i32, P_i32,
                                             P_i64, P_i64, P_i64, P_i64, P_i64, P_i64]),
     "cse_layout_offsets_count": (C.c_int64, [C.c_int64, P_pb, C.c_int64, P_i64, P_i32, P_i32]),
+    "cse_register_functor": (C.c_int, [C.c_void_p, P_i32]),
+    "cse_functor_shape": (C.c_int, [C.c_int32, P_i32, P_i32, P_i32, P_i32]),
     "cse_abi_version": (C.c_int, []),
     "cse_build_info": (C.c_char_p, []),
 }
@@ -214,6 +222,29 @@ def lib():
 
 def last_error():
     return lib().cse_last_error().decode()
+
+
+def functor_shape(kind):
+    """(num_residuals, parameter block sizes, functor data size) of a built-in
+    or registered functor kind."""
+    if kind in FUNCTOR_SHAPES:
+        return FUNCTOR_SHAPES[kind]
+    nr, nb, d = C.c_int32(), C.c_int32(), C.c_int32()
+    sizes = (C.c_int32 * MAX_PARAMETER_BLOCKS)()
+    check(lib().cse_functor_shape(int(kind), C.byref(nr), C.byref(nb), sizes, C.byref(d)),
+          "cse_functor_shape")
+    shape = (nr.value, tuple(sizes[:nb.value]), d.value)
+    FUNCTOR_SHAPES[kind] = shape
+    return shape
+
+
+def load_functor_library(path):
+    """Load a user functor library (a hipcc-built .so that includes
+    ceres_amd/autodiff_cuda.h and links libcse.so) after libcse.so itself, so
+    that its cse_register_functor calls reach this process's registry (the
+    library binds to the loaded copy through libcse.so's SONAME)."""
+    lib()
+    return C.CDLL(os.path.abspath(path))
 
 
 def check(rc, what):

@@ -26,7 +26,7 @@ from typing import List, Optional
 import numpy as np
 
 from . import _cse
-from ._cse import FUNCTOR_SHAPES
+from ._cse import FUNCTOR_SHAPES, functor_shape
 
 BLOCK_SPARSE = "block_sparse"
 COMPRESSED_ROW = "compressed_row"
@@ -45,6 +45,9 @@ class Loss:
     a: float = 1.0
     scaled: bool = False
     scale: float = 1.0
+    # LOSS_USER: the user loss object's bytes (cse_loss.user), as produced by
+    # the functor library that compiled the loss.
+    user: bytes = b""
 
     @staticmethod
     def trivial():
@@ -58,8 +61,27 @@ class Loss:
     def cauchy(a):
         return Loss(_cse.LOSS_CAUCHY, float(a))
 
+    @staticmethod
+    def user_loss(obj_bytes):
+        """A user LossFunctionCUDA (CSE_LOSS_USER): its object bytes; only
+        with a user functor kind registered with that loss type."""
+        b = bytes(obj_bytes)
+        if len(b) > _cse.USER_LOSS_BYTES:
+            raise ValueError("user loss object larger than 64 bytes")
+        return Loss(_cse.LOSS_USER, 0.0, False, 1.0, b)
+
     def scaled_by(self, s):
-        return Loss(self.kind, self.a, True, float(s))
+        return Loss(self.kind, self.a, True, float(s), self.user)
+
+    def key(self):
+        return (self.kind, self.a, self.scaled, self.scale, self.user)
+
+    def describe(self):
+        """The cse_loss of this loss."""
+        d = _cse.cse_loss(self.kind, int(self.scaled), self.a, self.scale)
+        if self.user:
+            C.memmove(C.addressof(d.user), self.user, len(self.user))
+        return d
 
 
 @dataclass
@@ -123,12 +145,12 @@ class Program:
         nres = np.zeros(self.num_residual_blocks, np.int32)
         for g in self.groups:
             idx = g.index if g.index is not None else np.arange(g.first, g.first + g.n)
-            nres[idx] = FUNCTOR_SHAPES[g.kind][0]
+            nres[idx] = functor_shape(g.kind)[0]
         return nres
 
     @property
     def num_residuals(self):
-        return int(sum(FUNCTOR_SHAPES[g.kind][0] * g.n for g in self.groups))
+        return int(sum(functor_shape(g.kind)[0] * g.n for g in self.groups))
 
     def block_params_csr(self):
         """(param_begin[nrb+1], param_ids) in program order."""
@@ -260,7 +282,7 @@ class Program:
             idx = None if g.index is None else np.ascontiguousarray(g.index, np.int64)
             keep += [ids, data, idx]
             groups[k].functor_kind = g.kind
-            groups[k].loss = _cse.cse_loss(g.loss.kind, int(g.loss.scaled), g.loss.a, g.loss.scale)
+            groups[k].loss = g.loss.describe()
             groups[k].num_blocks = g.n
             groups[k].residual_block_index = _ptr(idx, C.c_int64)
             groups[k].first_residual_block = g.first
@@ -350,7 +372,7 @@ class ProblemCUDA:
         self._manifold[b] = _cse.MANIFOLD_QUATERNION_EUCLIDEAN
 
     def add_residual_blocks(self, kind, loss, ids, data):
-        ids = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1, len(FUNCTOR_SHAPES[kind][1])))
+        ids = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1, len(functor_shape(kind)[1])))
         data = np.ascontiguousarray(np.asarray(data, np.float64).reshape(ids.shape[0], -1))
         n = ids.shape[0]
         self._groups.append(ResidualGroup(kind, loss or Loss.trivial(), ids, data, None, self._nrb))
@@ -383,7 +405,7 @@ class ProblemCUDA:
         if group_by_type:
             merged = {}
             for g in groups:
-                key = (g.kind, g.loss.kind, g.loss.a, g.loss.scaled, g.loss.scale)
+                key = (g.kind,) + g.loss.key()
                 idx = np.arange(g.first, g.first + g.n, dtype=np.int64)
                 if key in merged:
                     m = merged[key]
@@ -560,11 +582,18 @@ class Evaluator:
     def wait(self):
         return _cse.check(_cse.lib().cse_wait(self.handle), "cse_wait")
 
-    def plus(self, state, delta):
-        """Evaluator::Plus (program.cc:121-149) on the GPU, host arrays."""
+    def plus(self, state, delta, out=None):
+        """Evaluator::Plus (program.cc:121-149) on the GPU, host arrays.
+        out: the result array (C-contiguous float64, the state's size); it may
+        be `state` itself (Plus(x, delta, x), as Ceres' line search and
+        dogleg steps call it)."""
         state = np.ascontiguousarray(state, np.float64)
         delta = np.ascontiguousarray(delta, np.float64)
-        out = np.empty_like(state)
+        if out is None:
+            out = np.empty_like(state)
+        elif (not isinstance(out, np.ndarray) or out.dtype != np.float64 or
+              not out.flags.c_contiguous or out.size != state.size):
+            raise ValueError("plus: out must be a C-contiguous float64 array of the state's size")
         _cse.check(_cse.lib().cse_plus(self.handle, _ptr(state, C.c_double),
                                        _ptr(delta, C.c_double), _ptr(out, C.c_double)), "cse_plus")
         return out

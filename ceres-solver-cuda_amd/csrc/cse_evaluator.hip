@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -26,6 +27,7 @@
 #include "../../include/cse.h"
 #include "group_store_kernel.hpp"
 #include "jet_kernels.h"
+#include "launch.hpp"
 #include "multi_device.h"
 #include "schur_kernels.hpp"
 #ifdef CSE_TUNING
@@ -93,7 +95,36 @@ bool VisitKind(int kind, F&& f) {
 }
 
 // Known-answer-test kinds: general path and trivial loss only.
-bool IsTestKind(int kind) { return kind >= 100; }
+bool IsTestKind(int kind) { return kind >= 100 && kind < CSE_FUNCTOR_USER_FIRST; }
+
+// ---- User functor kinds (cse_register_functor): the kernels live in the
+// user's TU (include/ceres_amd/autodiff_cuda.h); the library holds their
+// launch tables.  Entries are never removed, so a pointer to one stays valid.
+struct UserKindEntry {
+  cse_functor_ops ops;
+  std::string name;
+};
+std::mutex g_user_mu;
+std::vector<UserKindEntry*> g_user_kinds;
+
+const cse_functor_ops* UserOps(int kind) {
+  if (kind < CSE_FUNCTOR_USER_FIRST) return nullptr;
+  std::lock_guard<std::mutex> lock(g_user_mu);
+  const size_t i = (size_t)(kind - CSE_FUNCTOR_USER_FIRST);
+  return i < g_user_kinds.size() ? &g_user_kinds[i]->ops : nullptr;
+}
+
+bool IsUserKind(int kind) { return UserOps(kind) != nullptr; }
+
+// Every affine kernel of a user kind present (the header builds all eight
+// or none).
+bool UserAffine(const cse_functor_ops* u) {
+  bool all = true;
+  for (int c = 0; c < 2; ++c)
+    for (int j = 0; j < 2; ++j)
+      for (int d = 0; d < 2; ++d) all = all && u->affine[c][j][d] != nullptr;
+  return all;
+}
 
 struct KindShape {
   int nr = 0, nb = 0, data = 0;
@@ -103,6 +134,17 @@ struct KindShape {
 };
 
 bool ShapeOf(int kind, KindShape* k) {
+  if (const cse_functor_ops* u = UserOps(kind)) {
+    *k = KindShape{};
+    k->nr = u->num_residuals;
+    k->nb = u->num_parameter_blocks;
+    k->data = u->data_size;
+    for (int j = 0; j < k->nb; ++j) k->sz[j] = u->parameter_block_sizes[j];
+    k->s0 = k->sz[0];
+    k->s1 = k->nb > 1 ? k->sz[1] : 0;
+    k->x0 = k->s0;
+    return true;
+  }
   return VisitKind(kind, [&](auto kd) {
     using K = decltype(kd);
     using Tr = cse::KindTraits<K>;
@@ -165,6 +207,8 @@ struct DevBuf {
 
 struct Group {
   int kind = 0;
+  const cse_functor_ops* user = nullptr;  // a registered user functor kind
+  std::string user_name;
   KindShape shape{};
   cse_loss loss{};
   int64_t n = 0;
@@ -1085,39 +1129,36 @@ int BuildGradPlan(const cse_residual_group& g, const KindShape& k, int j, Group:
   return CSE_OK;
 }
 
-template <int NR, int S>
-void LaunchGradSlot(const cse::GradArgs& ga, const Group::GradPlan& P, hipStream_t s) {
-  if (ga.perm == nullptr) {  // identity order: contiguous block ranges (points)
-    hipLaunchKernelGGL((cse::GradientRangeKernel<NR, S>),
-                       dim3((unsigned)((ga.count + cse::kWave - 1) / cse::kWave)), dim3(cse::kWave),
-                       0, s, ga);
-  } else if (P.wave) {  // many blocks per parameter block (cameras): chunks
-    const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
-    const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
-    if (P.nchunks > 0)
-      hipLaunchKernelGGL((cse::GradientLanesKernel<NR, S>), grid, dim3(cse::kBlockThreads), 0, s,
-                         ga, ch);
-    hipLaunchKernelGGL((cse::GradientChunkReduceKernel<S>),
-                       dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                       dim3(cse::kBlockThreads), 0, s, ga, ch);
-  } else {
-    hipLaunchKernelGGL((cse::GradientSlotKernel<NR, S, false>),
-                       dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                       dim3(cse::kBlockThreads), 0, s, ga);
-  }
+// The post-pass form of a plan (cse::GradForm) and its chunk table.
+int GradFormOf(const cse::GradArgs& ga, const Group::GradPlan& P) {
+  if (ga.perm == nullptr) return cse::kGradRange;  // identity order: contiguous ranges (points)
+  return P.wave ? cse::kGradChunked : cse::kGradPerBlock;  // many blocks per parameter block: chunks
+}
+cse::GradChunks GradChunksOf(const Group::GradPlan& P) {
+  return cse::GradChunks{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
 }
 
-bool GradSupported(int nr, int size) {
+// Gradient post-pass kernels of the built-in shapes; a user kind brings its
+// own (cse_functor_ops.gradient).
+bool GradSupported(int nr, int size, const cse_functor_ops* user = nullptr, int slot = 0) {
+  if (user) return user->gradient[slot] != nullptr;
   return (nr == 2 && (size == 9 || size == 3 || size == 7 || size == 10)) || (nr == 3 && size == 3);
 }
 
 bool LaunchGradPass(int nr, int size, const cse::GradArgs& ga, const Group::GradPlan& P,
-                    hipStream_t s) {
-  if (nr == 2 && size == 9) return LaunchGradSlot<2, 9>(ga, P, s), true;
-  if (nr == 2 && size == 3) return LaunchGradSlot<2, 3>(ga, P, s), true;
-  if (nr == 2 && size == 7) return LaunchGradSlot<2, 7>(ga, P, s), true;
-  if (nr == 2 && size == 10) return LaunchGradSlot<2, 10>(ga, P, s), true;
-  if (nr == 3 && size == 3) return LaunchGradSlot<3, 3>(ga, P, s), true;
+                    hipStream_t s, const cse_functor_ops* user = nullptr, int slot = 0) {
+  const int form = GradFormOf(ga, P);
+  const cse::GradChunks ch = GradChunksOf(P);
+  if (user) {
+    if (!user->gradient[slot]) return false;
+    user->gradient[slot](&ga, &ch, form, s);
+    return true;
+  }
+  if (nr == 2 && size == 9) return cse::LaunchGradientSlot<2, 9>(ga, ch, form, s), true;
+  if (nr == 2 && size == 3) return cse::LaunchGradientSlot<2, 3>(ga, ch, form, s), true;
+  if (nr == 2 && size == 7) return cse::LaunchGradientSlot<2, 7>(ga, ch, form, s), true;
+  if (nr == 2 && size == 10) return cse::LaunchGradientSlot<2, 10>(ga, ch, form, s), true;
+  if (nr == 3 && size == 3) return cse::LaunchGradientSlot<3, 3>(ga, ch, form, s), true;
   return false;
 }
 
@@ -1125,8 +1166,11 @@ int DetectAffine(const cse_problem_desc* d, const cse_residual_group& g, const K
                   Group* G) {
   const int64_t n = g.num_blocks;
   if (n == 0) return kTable;
-  // The affine kernels take one or two slots, at most three residuals.
+  // The affine kernels take one or two slots, at most three residuals; a
+  // user kind has them only for the shapes its header instantiates.
   if (k.nb > 2 || k.nr > 3 || IsTestKind(g.functor_kind)) return kTable;
+  if (const cse_functor_ops* u = UserOps(g.functor_kind))
+    if (!UserAffine(u)) return kTable;
   auto gidx = [&](int64_t i) {
     return g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i;
   };
@@ -1365,6 +1409,8 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.loss.a = G.loss.a;
   a.loss.scale = G.loss.scale;
   a.loss.scaled = G.loss.scaled;
+  static_assert(sizeof(a.user_loss) == sizeof(G.loss.user), "user loss bytes");
+  std::memcpy(a.user_loss, G.loss.user, sizeof(a.user_loss));
   a.apply_loss = ev->opts.apply_loss_function;
   a.check_finite = ev->opts.check_finite;
   a.num_cus = ev->num_cus;
@@ -1679,11 +1725,19 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
     Group& G = ev->groups[g];
     if (G.n == 0) continue;
     const bool dma = G.packed0.p != nullptr;
-    LaunchFn fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma, G.const0);
-    if (G.jet && jets)  // the Jet<double, 12> instantiations (cse_create kept only these shapes)
-      fn = G.policy == kTable ? cse::JetSnavelyTable(G.loss.kind)
-                              : cse::JetSnavelyJacobian(G.loss.kind, G.policy == kAffineCrs);
-    if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
+    LaunchFn fn = nullptr;
+    cse_kernel_launch_fn ufn = nullptr;  // a user kind's kernel (its own TU)
+    if (G.user) {
+      ufn = G.policy == kTable ? G.user->table[jets ? 1 : 0]
+                               : G.user->affine[G.policy == kAffineCrs][jets ? 1 : 0][dma ? 1 : 0];
+      if (!ufn) return Fail(CSE_ERR_UNSUPPORTED, "user functor kind " + G.user_name + " has no such kernel");
+    } else {
+      fn = Pick(G.kind, G.loss.kind, jets, G.policy, dma, G.const0);
+      if (G.jet && jets)  // the Jet<double, 12> instantiations (cse_create kept only these shapes)
+        fn = G.policy == kTable ? cse::JetSnavelyTable(G.loss.kind)
+                                : cse::JetSnavelyJacobian(G.loss.kind, G.policy == kAffineCrs);
+      if (!fn) return Fail(CSE_ERR_UNSUPPORTED, "no kernel for functor kind " + std::to_string(G.kind));
+    }
     // Gradient: a deterministic post-pass over the written residuals and
     // Jacobian when the group has plans for all its slots, else in-kernel
     // FP64 atomics (as the reference).
@@ -1743,7 +1797,10 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
         }
       }
     }
-    fn(a, G.num_wg, ev->stream);
+    if (ufn)
+      ufn(&a, G.num_wg, ev->stream);
+    else
+      fn(a, G.num_wg, ev->stream);
     CSE_HIP(hipGetLastError());
     if (G.const0 && jets && d_jac && G.side.p) {
       // The 64-byte sectors two held-camera chunks share (the full chunks
@@ -1791,7 +1848,7 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
         ga.lo = P.lo;
         ga.grad = d_grad;
         ga.delta_base = G.delta_base[j];
-        if (!LaunchGradPass(G.shape.nr, sizes[j], ga, P, ev->stream))
+        if (!LaunchGradPass(G.shape.nr, sizes[j], ga, P, ev->stream, G.user, j))
           return Fail(CSE_ERR_UNSUPPORTED, "no gradient pass for this shape");
         CSE_HIP(hipGetLastError());
       }
@@ -1924,10 +1981,26 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     Group G;
     if (g.functor_kind < 0 || !ShapeOf(g.functor_kind, &G.shape))
       return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown functor kind " + std::to_string(g.functor_kind)));
-    if (g.loss.kind < CSE_LOSS_TRIVIAL || g.loss.kind > CSE_LOSS_CAUCHY)
+    if (g.loss.kind < CSE_LOSS_TRIVIAL || g.loss.kind > CSE_LOSS_USER)
       return bail(Fail(CSE_ERR_UNSUPPORTED, "unknown loss kind " + std::to_string(g.loss.kind)));
     if (IsTestKind(g.functor_kind) && (g.loss.kind != CSE_LOSS_TRIVIAL || g.loss.scaled))
       return bail(Fail(CSE_ERR_UNSUPPORTED, "test functor kinds take the trivial loss only"));
+    G.user = UserOps(g.functor_kind);
+    if (G.user) {
+      // The kernels of a user kind apply the loss they were built with
+      // (AutoDiffResidualBlockCUDAEvaluator<F, LossFunctionCUDA, ...>).
+      {
+        std::lock_guard<std::mutex> lock(g_user_mu);
+        G.user_name = g_user_kinds[(size_t)(g.functor_kind - CSE_FUNCTOR_USER_FIRST)]->name;
+      }
+      if (g.loss.kind != G.user->loss_kind)
+        return bail(Fail(CSE_ERR_INVALID, "group " + std::to_string(gi) + ": user functor kind " +
+                                              G.user_name + " was registered with loss kind " +
+                                              std::to_string(G.user->loss_kind) + ", the group has " +
+                                              std::to_string(g.loss.kind)));
+    } else if (g.loss.kind == CSE_LOSS_USER) {
+      return bail(Fail(CSE_ERR_INVALID, "the user loss kind (3) needs a user functor kind registered with it"));
+    }
     if (g.num_blocks < 0 || (g.num_blocks > 0 && (!g.parameter_block_ids || !g.functor_data)))
       return bail(Fail(CSE_ERR_INVALID, "group " + std::to_string(gi) + " arrays missing"));
     G.kind = g.functor_kind;
@@ -2081,10 +2154,10 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     if (G.affine && ev->has_layout) {
       const int sizes[2] = {k.s0, k.s1};
       for (int j = 0; j < k.nb; ++j)
-        if (GradSupported(k.nr, sizes[j]) &&
+        if (GradSupported(k.nr, sizes[j], G.user, j) &&
             (rc = BuildGradPlan(g, k, j, &G.grad[j], s,
                                 j == 0 && G.const0 ? d->parameter_blocks : nullptr,
-                                j == 0 && k.nb == 2 ? CamGradPasses(g, k) : 1)))
+                                j == 0 && k.nb == 2 && FusedKind(G.kind) ? CamGradPasses(g, k) : 1)))
           return bail(rc);
     }
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
@@ -2251,28 +2324,10 @@ int cse_set_plus_jacobians(cse_evaluator* ev, const double* plus_jacobians) {
 extern "C++" {
 namespace {
 
-template <class K>
-void LaunchMultiply(const cse::GroupArgs& a, bool affine, bool left, const double* x, double* y,
-                    hipStream_t s) {
-  const dim3 grid((unsigned)((a.n + cse::kBlockThreads - 1) / cse::kBlockThreads));
-  if constexpr (cse::KindTraits<K>::NB <= 2) {
-    if (affine && !left) {
-      hipLaunchKernelGGL(cse::RightMultiplyAffineKernel<K>, grid, dim3(cse::kBlockThreads), 0, s,
-                         a, x, y);
-      return;
-    }
-  }
-  if (left)
-    hipLaunchKernelGGL((cse::MultiplyTableKernel<K, true>), grid, dim3(cse::kBlockThreads), 0, s,
-                       a, x, y);
-  else
-    hipLaunchKernelGGL((cse::MultiplyTableKernel<K, false>), grid, dim3(cse::kBlockThreads), 0, s,
-                       a, x, y);
-}
-
 bool DispatchMultiply(int kind, const cse::GroupArgs& a, bool affine, bool left, const double* x,
                       double* y, hipStream_t s) {
-  return VisitKind(kind, [&](auto kd) { LaunchMultiply<decltype(kd)>(a, affine, left, x, y, s); });
+  const int which = affine && !left ? 0 : left ? 2 : 1;
+  return VisitKind(kind, [&](auto kd) { cse::LaunchMultiplyKernel<decltype(kd)>(a, which, x, y, s); });
 }
 
 int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double* y, bool left) {
@@ -2307,13 +2362,17 @@ int JacobianMultiply(cse_evaluator* ev, const double* J, const double* x, double
         ga.lo = P.lo;
         ga.grad = y;
         ga.delta_base = G.delta_base[j];
-        if (!LaunchGradPass(G.shape.nr, sizes[j], ga, P, ev->stream))
+        if (!LaunchGradPass(G.shape.nr, sizes[j], ga, P, ev->stream, G.user, j))
           return Fail(CSE_ERR_UNSUPPORTED, "no J^T x pass for this shape");
       }
     } else {
       if (!G.affine && !ev->any_general)
         return Fail(CSE_ERR_UNSUPPORTED, "table-path tables were not uploaded");
-      if (!DispatchMultiply(G.kind, a, affine, left, x, y, ev->stream))
+      if (G.user) {
+        if (!G.user->multiply)
+          return Fail(CSE_ERR_UNSUPPORTED, "user functor kind " + G.user_name + " has no multiply kernel");
+        G.user->multiply(&a, affine && !left ? 0 : left ? 2 : 1, x, y, ev->stream);
+      } else if (!DispatchMultiply(G.kind, a, affine, left, x, y, ev->stream))
         return Fail(CSE_ERR_UNSUPPORTED, "no multiply kernel for functor kind " +
                                              std::to_string(G.kind));
     }
@@ -2705,6 +2764,72 @@ int cse_shard_transfer_bytes(cse_evaluator* ev, int64_t* state_h2d_bytes, int64_
 int cse_host_register(void* p, size_t bytes) { return CseHostRegister(p, bytes); }
 
 int cse_host_unregister(void* p) { return CseHostUnregister(p); }
+
+// Registration compares whole tables bytewise: no padding inside.
+static_assert(offsetof(cse_functor_ops, kernel_args_tag) == 80 && sizeof(cse_functor_ops) == 200,
+              "cse_functor_ops layout");
+
+int cse_register_functor(const cse_functor_ops* ops, int32_t* kind) {
+  if (!ops || !kind) return Fail(CSE_ERR_INVALID, "null functor table or kind");
+  const std::string name = ops->name ? ops->name : "(unnamed)";
+  if (ops->abi_version != CSE_ABI_VERSION)
+    return Fail(CSE_ERR_INVALID, "functor " + name + ": built against ABI " +
+                                     std::to_string(ops->abi_version) + ", the library is " +
+                                     std::to_string(CSE_ABI_VERSION));
+  if (ops->kernel_args_size != (int32_t)sizeof(cse::GroupArgs) ||
+      ops->gradient_args_size != (int32_t)sizeof(cse::GradArgs) ||
+      ops->kernel_args_tag != cse::kGroupArgsTag)
+    return Fail(CSE_ERR_INVALID, "functor " + name +
+                                     ": kernel argument layout differs from the library's (build "
+                                     "the functor against the same ceres-solver-cuda_amd headers)");
+  const int nb = ops->num_parameter_blocks;
+  if (ops->num_residuals < 1 || nb < 1 || nb > CSE_MAX_PARAMETER_BLOCKS || ops->data_size < 1)
+    return Fail(CSE_ERR_INVALID, "functor " + name + ": bad shape");
+  for (int j = 0; j < nb; ++j)
+    if (ops->parameter_block_sizes[j] < 1)
+      return Fail(CSE_ERR_INVALID, "functor " + name + ": parameter block size < 1");
+  if (ops->loss_kind < CSE_LOSS_TRIVIAL || ops->loss_kind > CSE_LOSS_USER ||
+      (ops->loss_kind == CSE_LOSS_USER &&
+       (ops->loss_size < 1 || ops->loss_size > CSE_USER_LOSS_BYTES)))
+    return Fail(CSE_ERR_INVALID, "functor " + name + ": bad loss kind or size");
+  if (!ops->table[0] || !ops->table[1])
+    return Fail(CSE_ERR_INVALID, "functor " + name + ": the general kernels are required");
+  bool any_affine = false;
+  for (int c = 0; c < 2; ++c)
+    for (int j = 0; j < 2; ++j)
+      for (int d = 0; d < 2; ++d) any_affine = any_affine || ops->affine[c][j][d];
+  if (any_affine && (!UserAffine(ops) || nb > 2 || ops->num_residuals > 3))
+    return Fail(CSE_ERR_INVALID, "functor " + name + ": affine kernels must come as all eight, "
+                                                     "for at most two blocks and three residuals");
+  std::lock_guard<std::mutex> lock(g_user_mu);
+  for (size_t i = 0; i < g_user_kinds.size(); ++i) {
+    const UserKindEntry& e = *g_user_kinds[i];
+    cse_functor_ops a = e.ops, b = *ops;
+    a.name = b.name = nullptr;
+    if (e.name == name && std::memcmp(&a, &b, sizeof(a)) == 0) {
+      *kind = CSE_FUNCTOR_USER_FIRST + (int32_t)i;
+      return CSE_OK;
+    }
+  }
+  UserKindEntry* e = new (std::nothrow) UserKindEntry{*ops, name};
+  if (!e) return Fail(CSE_ERR_OOM, "host allocation failed");
+  e->ops.name = nullptr;  // the copy in e->name serves
+  g_user_kinds.push_back(e);
+  *kind = CSE_FUNCTOR_USER_FIRST + (int32_t)(g_user_kinds.size() - 1);
+  return CSE_OK;
+}
+
+int cse_functor_shape(int32_t kind, int32_t* num_residuals, int32_t* num_parameter_blocks,
+                      int32_t* parameter_block_sizes, int32_t* data_size) {
+  KindShape k;
+  if (!ShapeOf(kind, &k)) return Fail(CSE_ERR_UNSUPPORTED, "unknown functor kind " + std::to_string(kind));
+  if (num_residuals) *num_residuals = k.nr;
+  if (num_parameter_blocks) *num_parameter_blocks = k.nb;
+  if (parameter_block_sizes)
+    for (int j = 0; j < k.nb; ++j) parameter_block_sizes[j] = k.sz[j];
+  if (data_size) *data_size = k.data;
+  return CSE_OK;
+}
 
 int cse_get_info(cse_evaluator* ev, cse_info* info) {
   if (!ev || !info) return Fail(CSE_ERR_INVALID, "null argument");

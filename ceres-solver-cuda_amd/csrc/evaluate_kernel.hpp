@@ -918,7 +918,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     ok = !bad;
   }
   const double cost =
-      LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr);
+      LossAndCorrect<K, kLoss, kJac>(a.loss, a.apply_loss, r, J0, J1, a.residuals != nullptr,
+                                     a.user_loss);
   bool act0 = true;  // slot-0 block active (T::kConst0: from its bit)
   if constexpr (T::kConst0) {
     static_assert(kCoop == 2, "constant slot-0 blocks: the repacked table");
@@ -1936,7 +1937,7 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const Group
         cost = 0.5 * sq;
       } else {
         double rho[3];
-        EvaluateLoss<kLoss>(a.loss, sq, rho);
+        EvaluateLoss<kLoss, K>(a.loss, sq, rho, a.user_loss);
         const Corrector corr(sq, rho);
         if constexpr (kJac) corr.template CorrectJacobian<NR, N>(r, J);
         corr.template CorrectResiduals<NR>(r);

@@ -96,7 +96,14 @@ struct GroupArgs {
   int check_finite;
   int num_cus;  // compute units of the device (persistent launches)
   unsigned long long* probe;  // tuning build: per-wave cycle accounting (pipeline kernel)
+  // kLossUser: the bytes of the group's loss object (cse_loss.user).
+  double user_loss[kUserLossDoubles];
 };
+
+// Layout tag of GroupArgs, checked when a user functor kind registers
+// kernels compiled in another TU (cse_register_functor): bump on any change
+// to the struct.
+constexpr uint64_t kGroupArgsTag = 0x6373654761310001ull;
 
 // Compile-time shape of a functor kind: kR residuals, NB parameter blocks
 // of sizes kSizes[0..NB) concatenated into N columns.
@@ -367,7 +374,7 @@ CSE_HD bool EvaluateFunctorFlat(const double* d, const double* x, double* r, dou
 // Jacobians nor residuals are output (residual_block.cc:175-179).
 template <class K, int kLoss, bool kJac>
 CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, double* J0,
-                             double* J1, bool correct = true) {
+                             double* J1, bool correct = true, const double* user_loss = nullptr) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p;
   double sq = 0.0;
@@ -376,7 +383,7 @@ CSE_HD double LossAndCorrect(const LossParams& lp, bool apply_loss, double* r, d
   const bool robust = (kLoss != kLossTrivial || lp.scaled) && apply_loss;
   if (!robust) return 0.5 * sq;
   double rho[3];
-  EvaluateLoss<kLoss>(lp, sq, rho);
+  EvaluateLoss<kLoss, K>(lp, sq, rho, user_loss);
   if (!kJac && !correct) return 0.5 * rho[0];
   const Corrector corr(sq, rho);
   if constexpr (kJac) {

@@ -7,12 +7,27 @@
 #define CSE_LOSS_HPP_
 
 #include <cfloat>
+#include <type_traits>
 
 #include "jet.hpp"
 
 namespace cse {
 
-enum LossKind { kLossTrivial = 0, kLossHuber = 1, kLossCauchy = 2 };
+// kLossUser: a LossFunctionCUDA type compiled into a user-registered
+// functor kind (include/ceres_amd/autodiff_cuda.h); its state travels as
+// kUserLossDoubles doubles of bytes (GroupArgs::user_loss).
+enum LossKind { kLossTrivial = 0, kLossHuber = 1, kLossCauchy = 2, kLossUser = 3 };
+constexpr int kUserLossDoubles = 8;
+
+// The loss type a kind carries for kLossUser (K::UserLoss), else void.
+template <class K, class = void>
+struct UserLossOf {
+  using type = void;
+};
+template <class K>
+struct UserLossOf<K, decltype((void)sizeof(typename K::UserLoss))> {
+  using type = typename K::UserLoss;
+};
 
 struct LossParams {
   double a;
@@ -20,10 +35,20 @@ struct LossParams {
   int scaled;
 };
 
-// rho(s) = (rho0, rho1, rho2).
-template <int kLoss>
-CSE_HD void EvaluateLoss(const LossParams& lp, double s, double rho[3]) {
-  if constexpr (kLoss == kLossHuber) {
+// rho(s) = (rho0, rho1, rho2).  kLossUser: K's UserLoss object, rebuilt
+// from its bytes (user), evaluates rho (its Evaluate(s, rho), the
+// LossFunctionCUDA contract of include/ceres/loss_function_cuda.h:62-94).
+template <int kLoss, class K = void>
+CSE_HD void EvaluateLoss(const LossParams& lp, double s, double rho[3],
+                         const double* user = nullptr) {
+  if constexpr (kLoss == kLossUser) {
+    using UL = typename UserLossOf<K>::type;
+    static_assert(!std::is_void<UL>::value, "kLossUser needs a kind with a UserLoss type");
+    static_assert(sizeof(UL) <= kUserLossDoubles * sizeof(double), "user loss too large");
+    alignas(UL) unsigned char buf[sizeof(UL)];
+    __builtin_memcpy(buf, user, sizeof(UL));
+    reinterpret_cast<const UL*>(buf)->Evaluate(s, rho);
+  } else if constexpr (kLoss == kLossHuber) {
     const double a = lp.a, b = a * a;
     if (s > b) {
       // loss_function_cuda.h:72-87 with one division: 1/r serves rho1 and

@@ -6,12 +6,19 @@
 // (Evaluate(state, cost, residuals, gradient, jacobian_values)), on top of
 // the C ABI in include/cse.h.  Header-only; link libcse.so.
 //
+// Residual functors: AddResidualBlock<F, kR, Ns...> takes any
+// AutoDiffCostFunction-style functor (template <typename T> bool
+// operator()(const T*..., T*) const), by value or wrapped in an
+// AutoDiffCostFunction<F, kR, Ns...>, as the reference does
+// (problem_cuda.h:110-160,423-474).  The library's own kinds
+// (SnavelyReprojectionError, ...WithQuaternions, ...NoRadialDistortion,
+// PointDisplacementError below) are pre-instantiated in libcse.so and work
+// from any C++ compiler; any other functor has its kernels instantiated in
+// the caller's TU, which must then be compiled with hipcc for gfx950 and
+// include ceres_amd/autodiff_cuda.h (the reference likewise compiles user
+// functors with nvcc, README.md:19-33).
+//
 // Differences from the reference, on purpose:
-//  * the residual functors are the library's pre-instantiated gfx950
-//    kernels (SnavelyReprojectionError, ...WithQuaternions,
-//    ...NoRadialDistortion, PointDisplacementError): AddResidualBlock takes
-//    the functor object itself instead of a ceres::CostFunction* it would
-//    dynamic_cast (problem_cuda.h:443-450);
 //  * manifolds are given by their PlusJacobian (the only thing the
 //    evaluator uses, cuda_evaluator_kernel.h:355-371), recomputed from the
 //    current state on every Evaluate;
@@ -19,6 +26,7 @@
 #ifndef CERES_AMD_PROBLEM_CUDA_H_
 #define CERES_AMD_PROBLEM_CUDA_H_
 
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -37,7 +45,12 @@
 namespace ceres_amd {
 
 // ---------------------------------------------------------------------------
-// Loss functions (include/ceres/loss_function_cuda.h:62-150).
+// Loss functions (include/ceres/loss_function_cuda.h:62-150).  The library's
+// three are described to the C ABI by kind and parameter; any other class
+// with __host__ __device__ void Evaluate(double s, double rho[3]) const is a
+// user loss (CSE_LOSS_USER): it is compiled into the user functor kind's
+// kernels and its object travels as bytes (trivially copyable, at most
+// CSE_USER_LOSS_BYTES).
 // ---------------------------------------------------------------------------
 struct TrivialLossCUDA {
   cse_loss Describe() const { return cse_loss{CSE_LOSS_TRIVIAL, 0, 1.0, 1.0}; }
@@ -52,17 +65,50 @@ struct CauchyLossCUDA {
   cse_loss Describe() const { return cse_loss{CSE_LOSS_CAUCHY, 0, a, 1.0}; }
   double a;
 };
+template <typename L, typename = void>
+struct HasDescribe : std::false_type {};
+template <typename L>
+struct HasDescribe<L, decltype((void)std::declval<const L&>().Describe())> : std::true_type {};
+
+// The C-ABI description of a loss object (library or user loss).
+template <typename L>
+cse_loss DescribeLoss(const L& loss) {
+  if constexpr (HasDescribe<L>::value) {
+    return loss.Describe();
+  } else {
+    static_assert(std::is_trivially_copyable<L>::value && sizeof(L) <= CSE_USER_LOSS_BYTES,
+                  "a user LossFunctionCUDA must be trivially copyable and at most 64 bytes");
+    cse_loss l{};
+    l.kind = CSE_LOSS_USER;
+    l.a = 0.0;
+    l.scale = 1.0;
+    std::memcpy(l.user, &loss, sizeof(L));
+    return l;
+  }
+}
+
 template <typename LossFunctionCUDA>
 struct ScaledLossCUDA {
   ScaledLossCUDA(const LossFunctionCUDA& rho, double a) : rho(rho), a(a) {}
   cse_loss Describe() const {
-    cse_loss l = rho.Describe();
+    cse_loss l = DescribeLoss(rho);
     l.scaled = 1;
     l.scale = a;
     return l;
   }
   LossFunctionCUDA rho;
   double a;
+};
+
+// The loss the kernels are compiled for: ScaledLossCUDA<L> applies L's rho
+// and scales at run time (cse_loss.scaled), so its kernels are L's.
+template <typename L>
+struct BaseLoss {
+  using type = L;
+};
+template <typename L>
+struct BaseLoss<ScaledLossCUDA<L>> {
+  using type = typename BaseLoss<L>::type;
 };
 
 // ---------------------------------------------------------------------------
@@ -100,6 +146,34 @@ struct PointDisplacementError {  // evaluator_cuda_test.cu.cc:84-110
 // Shape of each kind, checked against the template arguments of
 // AddResidualBlock<F, kNumResiduals, Ns...>.
 template <typename F> struct FunctorShape;
+// A functor type the library has pre-instantiated (it carries kKind).
+template <typename F, typename = void>
+struct IsLibraryFunctor : std::false_type {};
+template <typename F>
+struct IsLibraryFunctor<F, decltype((void)F::kKind)> : std::true_type {};
+template <typename L>
+constexpr bool kIsLibraryLoss = HasDescribe<typename BaseLoss<L>::type>::value;
+
+// The functor kind of a user functor type with loss type L: defined by
+// ceres_amd/autodiff_cuda.h (hipcc TUs only), which instantiates and
+// registers the kernels (cse_register_functor) on first use.  A TU without
+// that header can add residual blocks of the library's kinds only.
+template <typename F, typename L, int kNumResiduals, int... Ns>
+struct UserFunctorKind;
+
+// AutoDiffCostFunction<F, kNumResiduals, Ns...> (include/ceres/
+// autodiff_cost_function.h): owns the functor; ProblemCUDA::AddResidualBlock
+// takes it as the reference's takes its CostFunction* (problem_cuda.h:
+// 443-450) and owns it afterwards.
+template <typename CostFunctor, int kNumResiduals, int... Ns>
+class AutoDiffCostFunction {
+ public:
+  explicit AutoDiffCostFunction(CostFunctor* functor) : functor_(functor) {}
+  const CostFunctor& functor() const { return *functor_; }
+
+ private:
+  std::unique_ptr<CostFunctor> functor_;
+};
 template <> struct FunctorShape<SnavelyReprojectionError> {
   static constexpr int kR = 2, kData = 2; static constexpr int kSizes[2] = {9, 3}; static constexpr int kNb = 2;
 };
@@ -234,23 +308,57 @@ class ProblemCUDA {
             typename... Ts>
   ResidualBlockId AddResidualBlock(const CostFunctor& functor, const LossFunctionCUDA* loss,
                                    double* x0, Ts*... xs) {
-    using S = FunctorShape<CostFunctor>;
-    static_assert(S::kR == kNumResiduals, "kNumResiduals does not match the functor");
-    static_assert(sizeof...(Ns) == S::kNb, "parameter block count does not match the functor");
     static_assert(sizeof...(Ts) + 1 == sizeof...(Ns), "one pointer per parameter block");
+    static_assert(kNumResiduals >= 1, "the number of residuals must be static");
     constexpr int sizes[] = {Ns...};
-    for (int j = 0; j < S::kNb; ++j)
-      if (sizes[j] != S::kSizes[j]) throw std::invalid_argument("parameter block size mismatch");
     double* ptrs[] = {x0, xs...};
     Residual res;
-    res.kind = CostFunctor::kKind;
-    res.loss = loss ? loss->Describe() : TrivialLossCUDA().Describe();
     res.nres = kNumResiduals;
-    for (int j = 0; j < S::kNb; ++j) res.blocks.push_back(Block(ptrs[j], sizes[j]));
-    res.data.resize(S::kData);
-    functor.Pack(res.data.data());
+    if constexpr (IsLibraryFunctor<CostFunctor>::value && kIsLibraryLoss<LossFunctionCUDA>) {
+      // A kind pre-instantiated in libcse.so.
+      using S = FunctorShape<CostFunctor>;
+      static_assert(S::kR == kNumResiduals, "kNumResiduals does not match the functor");
+      static_assert(sizeof...(Ns) == S::kNb, "parameter block count does not match the functor");
+      for (int j = 0; j < S::kNb; ++j)
+        if (sizes[j] != S::kSizes[j]) throw std::invalid_argument("parameter block size mismatch");
+      res.kind = CostFunctor::kKind;
+      res.data.resize(S::kData);
+      functor.Pack(res.data.data());
+    } else {
+      // Any other functor (or a library functor with a user loss): its
+      // kernels are instantiated in this TU (ceres_amd/autodiff_cuda.h).
+      // (An incomplete UserFunctorKind here means this TU lacks
+      // ceres_amd/autodiff_cuda.h, or is not compiled with hipcc.)
+      static_assert(!IsLibraryFunctor<CostFunctor>::value,
+                    "the library's functor kinds take the library's losses");
+      using U = UserFunctorKind<CostFunctor, typename BaseLoss<LossFunctionCUDA>::type,
+                                kNumResiduals, Ns...>;
+      res.kind = (cse_functor_kind)U::Kind();
+      res.data.assign(U::kDataSize, 0.0);
+      std::memcpy(res.data.data(), &functor, sizeof(CostFunctor));
+    }
+    res.loss = loss ? DescribeLoss(*loss) : TrivialLossCUDA().Describe();
+    for (int j = 0; j < (int)sizeof...(Ns); ++j) res.blocks.push_back(Block(ptrs[j], sizes[j]));
     residuals_.push_back(std::move(res));
     return (ResidualBlockId)residuals_.size() - 1;
+  }
+
+  // The reference's form (problem_cuda.h:110-144): a cost function wrapping
+  // the functor; the problem takes ownership of it.
+  template <typename CostFunctor, int kNumResiduals, int... Ns, typename LossFunctionCUDA,
+            typename... Ts>
+  ResidualBlockId AddResidualBlock(AutoDiffCostFunction<CostFunctor, kNumResiduals, Ns...>* cost,
+                                   const LossFunctionCUDA* loss, double* x0, Ts*... xs) {
+    cost_functions_.emplace_back(cost, [](void* p) {
+      delete static_cast<AutoDiffCostFunction<CostFunctor, kNumResiduals, Ns...>*>(p);
+    });
+    return AddResidualBlock<CostFunctor, kNumResiduals, Ns...>(cost->functor(), loss, x0, xs...);
+  }
+  template <typename CostFunctor, int kNumResiduals, int... Ns, typename... Ts>
+  ResidualBlockId AddResidualBlock(AutoDiffCostFunction<CostFunctor, kNumResiduals, Ns...>* cost,
+                                   std::nullptr_t, double* x0, Ts*... xs) {
+    return AddResidualBlock<CostFunctor, kNumResiduals, Ns...>(
+        cost, static_cast<const TrivialLossCUDA*>(nullptr), x0, xs...);
   }
 
   // nullptr loss = TrivialLossCUDA (problem_cuda.h:146-160).
@@ -335,6 +443,7 @@ class ProblemCUDA {
   std::map<double*, int> index_;
   std::vector<Residual> residuals_;
   std::vector<double*> elimination_;
+  std::vector<std::unique_ptr<void, void (*)(void*)>> cost_functions_;
 };
 
 // ---------------------------------------------------------------------------
@@ -501,10 +610,13 @@ class EvaluatorCUDA {
 
     // One group per (functor kind, loss): the per-type evaluator registry
     // (problem_cuda.h:462-468, registered_cuda_evaluators.cc:294-298).
-    std::map<std::tuple<int, int, double, int, double>, GroupStorage> groups;
+    using UserBytes = std::array<double, CSE_USER_LOSS_BYTES / 8>;
+    std::map<std::tuple<int, int, double, int, double, UserBytes>, GroupStorage> groups;
     for (int64_t i = 0; i < nrb; ++i) {
       const auto& R = problem_.residuals_[program_residuals_[i]];
-      auto key = std::make_tuple((int)R.kind, R.loss.kind, R.loss.a, R.loss.scaled, R.loss.scale);
+      UserBytes ub;
+      std::memcpy(ub.data(), R.loss.user, sizeof(ub));
+      auto key = std::make_tuple((int)R.kind, R.loss.kind, R.loss.a, R.loss.scaled, R.loss.scale, ub);
       GroupStorage& g = groups[key];
       g.g.functor_kind = R.kind;
       g.g.loss = R.loss;

@@ -29,8 +29,10 @@ extern "C" {
 /* 2: cse_parameter_block.manifold (was `reserved`, which had to be 0),
  *    cse_host_register / cse_host_unregister, cse_shard_transfer_bytes,
  *    shard-local state in cse_create_multi.
- * 3: cse_options.jacobian_form. */
-#define CSE_ABI_VERSION 3
+ * 3: cse_options.jacobian_form.
+ * 4: user functor kinds (cse_register_functor, cse_functor_shape),
+ *    CSE_LOSS_USER and cse_loss.user. */
+#define CSE_ABI_VERSION 4
 
 /* Return codes. */
 #define CSE_OK 0
@@ -85,14 +87,25 @@ typedef enum cse_functor_kind {
 typedef enum cse_loss_kind {
   CSE_LOSS_TRIVIAL = 0, /* TrivialLossCUDA (or nullptr, problem_cuda.h:146-160) */
   CSE_LOSS_HUBER = 1,   /* HuberLossCUDA(a) */
-  CSE_LOSS_CAUCHY = 2   /* CauchyLossCUDA(a) */
+  CSE_LOSS_CAUCHY = 2,  /* CauchyLossCUDA(a) */
+  /* A user LossFunctionCUDA type (a class with
+   *   __host__ __device__ void Evaluate(double s, double rho[3]) const,
+   * the contract of loss_function_cuda.h:62-94), compiled into a user functor
+   * kind's kernels (cse_functor_ops.loss_kind); the group's object is passed
+   * as bytes in cse_loss.user.  Only with such a kind. */
+  CSE_LOSS_USER = 3
 } cse_loss_kind;
+
+#define CSE_USER_LOSS_BYTES 64
 
 typedef struct cse_loss {
   int32_t kind;   /* cse_loss_kind */
   int32_t scaled; /* 1 = wrapped in ScaledLossCUDA(rho, scale) */
   double a;       /* loss parameter a */
   double scale;   /* ScaledLossCUDA factor */
+  /* CSE_LOSS_USER: the loss object's bytes (trivially copyable, at most
+   * CSE_USER_LOSS_BYTES), handed to the kernels as they are. */
+  double user[CSE_USER_LOSS_BYTES / 8];
 } cse_loss;
 
 /* One parameter block of the reduced Program; replaces ParameterBlockCUDA
@@ -265,6 +278,66 @@ int cse_evaluate_ex(cse_evaluator* ev, const double* state, double* cost,
 int cse_evaluate_device_ex(cse_evaluator* ev, const double* d_state, double* d_cost,
                            double* d_residuals, double* d_gradient,
                            double* d_jacobian_values, uint32_t flags);
+
+/* ---- User functor kinds -------------------------------------------------
+ * The reference evaluates any AutoDiffCostFunction functor: the user's nvcc
+ * TU instantiates EvaluateKernel<CostFunctor, LossFunctionCUDA, kR, Ns...>
+ * and ProblemCUDA::AddResidualBlock registers one
+ * AutoDiffResidualBlockCUDAEvaluator per such type
+ * (include/ceres/problem_cuda.h:423-474, README.md:19-33).  Here the user's
+ * hipcc TU instantiates this library's kernels for its functor
+ * (include/ceres_amd/autodiff_cuda.h, header-only: RegisterAutoDiffFunctor
+ * or ProblemCUDA::AddResidualBlock) and registers them as a table of launch
+ * functions; the kind returned is then used in cse_residual_group.
+ * functor_kind like a built-in one.  Kinds are process-wide and stay
+ * registered until the library is unloaded.
+ *
+ * The launch functions receive the library's kernel argument blocks, whose
+ * layout both sides take from the same headers (ceres-solver-cuda_amd/csrc/
+ * kernel_common.hpp, operator_kernels.hpp); kernel_args_size, gradient_args_size
+ * and kernel_args_tag must equal the library's or registration fails. */
+#define CSE_FUNCTOR_USER_FIRST 1000
+#define CSE_MAX_PARAMETER_BLOCKS 10
+
+/* Evaluation: kernel_args -> the group's arguments, stream = hipStream_t. */
+typedef void (*cse_kernel_launch_fn)(const void* kernel_args, int64_t num_workgroups, void* stream);
+/* which: 0 = y += J x on the affine layout, 1 = y += J x (general),
+ * 2 = y += J^T x (general). */
+typedef void (*cse_multiply_launch_fn)(const void* kernel_args, int32_t which, const double* x,
+                                       double* y, void* stream);
+/* The gradient post-pass of one slot; form 0 = identity order, 1 = chunked,
+ * 2 = one lane per parameter block. */
+typedef void (*cse_gradient_launch_fn)(const void* gradient_args, const void* chunks, int32_t form,
+                                       void* stream);
+
+typedef struct cse_functor_ops {
+  int32_t abi_version;          /* CSE_ABI_VERSION */
+  int32_t num_residuals;        /* kNumResiduals */
+  int32_t num_parameter_blocks; /* sizeof...(Ns) */
+  int32_t parameter_block_sizes[CSE_MAX_PARAMETER_BLOCKS];
+  int32_t data_size;            /* doubles of functor data per residual block */
+  int32_t loss_kind;            /* the cse_loss_kind the kernels apply; groups must match */
+  int32_t loss_size;            /* CSE_LOSS_USER: bytes of the loss object */
+  int32_t kernel_args_size;
+  int32_t gradient_args_size;
+  int32_t reserved[2];          /* 0 */
+  uint64_t kernel_args_tag;
+  const char* name;             /* copied; for messages and cse_functor_name */
+  cse_kernel_launch_fn table[2];        /* general kernel [0 residuals/cost, 1 + Jacobian] */
+  cse_kernel_launch_fn affine[2][2][2]; /* [CompressedRow][Jacobian][LDS-DMA gather]; NULL = none */
+  cse_multiply_launch_fn multiply;
+  cse_gradient_launch_fn gradient[2];   /* per slot of an affine kind; NULL = in-kernel atomics */
+} cse_functor_ops;
+
+/* Registers a user functor kind; *kind receives its number
+ * (>= CSE_FUNCTOR_USER_FIRST).  Registering the same table again (same name,
+ * shape and launch functions) returns the same kind. */
+int cse_register_functor(const cse_functor_ops* ops, int32_t* kind);
+
+/* Shape of a built-in or registered kind; parameter_block_sizes receives
+ * *num_parameter_blocks entries (room for CSE_MAX_PARAMETER_BLOCKS). */
+int cse_functor_shape(int32_t kind, int32_t* num_residuals, int32_t* num_parameter_blocks,
+                      int32_t* parameter_block_sizes, int32_t* data_size);
 
 /* Synchronises the evaluator's stream and returns the status of the most
  * recent evaluation (CSE_OK / CSE_EVALUATION_FAILED) or an error. */

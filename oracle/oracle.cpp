@@ -271,6 +271,27 @@ void PointDisplacement(const double* xyz, const T* point, T* residuals) {
   residuals[2] = std::fabs(xyz[2]) - jabs(point[2]);
 }
 
+// BundlerResidual (internal/ceres/bundle_adjustment_test_util.h:188-227):
+// Snavely's camera with the focal length applied before the perspective
+// division and the distortion after it.
+template <typename T>
+void BundlerResidual(const double* uv, const T* camera, const T* point, T* residuals) {
+  T p[3];
+  AngleAxisRotatePoint(camera, point, p);
+  p[0] = p[0] + camera[3];
+  p[1] = p[1] + camera[4];
+  p[2] = p[2] + camera[5];
+  const T& focal = camera[6];
+  const T& l1 = camera[7];
+  const T& l2 = camera[8];
+  const T xp = -focal * p[0] / p[2];
+  const T yp = -focal * p[1] / p[2];
+  const T r2 = xp * xp + yp * yp;
+  const T distortion = T(1.0) + r2 * (l1 + l2 * r2);
+  residuals[0] = distortion * xp - uv[0];
+  residuals[1] = distortion * yp - uv[1];
+}
+
 struct KindInfo {
   int num_residuals;
   int num_blocks;
@@ -284,6 +305,7 @@ static bool kind_info(int kind, KindInfo* k) {
     case ORACLE_SNAVELY_NO_DISTORTION_2_7_3: *k = {2, 2, {7, 3}, 2}; return true;
     case ORACLE_SNAVELY_QUATERNION_2_10_3: *k = {2, 2, {10, 3}, 2}; return true;
     case ORACLE_POINT_DISPLACEMENT_3_3: *k = {3, 1, {3, 0}, 3}; return true;
+    case ORACLE_BUNDLER_RESIDUAL_2_9_3: *k = {2, 2, {9, 3}, 2}; return true;
     default: return false;
   }
 }
@@ -334,6 +356,11 @@ static bool CostEvaluate(int kind, const double* data, const int32_t* sizes,
       return AutoDiff2<2, 10, 3>(
           [&](const Jet<13>* c, const Jet<13>* p, Jet<13>* r) { SnavelyQuaternion(data, c, p, r); },
           params, residuals, jacobians);
+    case ORACLE_BUNDLER_RESIDUAL_2_9_3:
+      if (!jacobians) { BundlerResidual<double>(data, params[0], params[1], residuals); return true; }
+      return AutoDiff2<2, 9, 3>(
+          [&](const Jet<12>* c, const Jet<12>* p, Jet<12>* r) { BundlerResidual(data, c, p, r); },
+          params, residuals, jacobians);
     case ORACLE_POINT_DISPLACEMENT_3_3:
       if (!jacobians) { PointDisplacement<double>(data, params[0], residuals); return true; }
       return AutoDiff2<3, 3, 0>(
@@ -367,8 +394,32 @@ static bool CostEvaluate(int kind, const double* data, const int32_t* sizes,
 // the host HuberLoss/CauchyLoss in internal/ceres/loss_function.cc:50-80).
 // ---------------------------------------------------------------------------
 static void Loss(int kind, double a, int scaled, double scale, double s,
-                 double rho[3]) {
+                 double rho[3], double b_param = 0.0) {
   switch (kind) {
+    case ORACLE_LOSS_SOFT_L_ONE: {  // loss_function.cc:66-73 (b = a^2, c = 1/b)
+      const double b = a * a, c = 1 / b;
+      const double sum = 1.0 + s * c;
+      const double tmp = std::sqrt(sum);
+      rho[0] = 2.0 * b * (tmp - 1.0);
+      rho[1] = std::max(std::numeric_limits<double>::min(), 1.0 / tmp);
+      rho[2] = -(c * rho[1]) / (2.0 * sum);
+      break;
+    }
+    case ORACLE_LOSS_TOLERANT: {  // loss_function.cc:87-118
+      const double bb = b_param, c = bb * std::log(1.0 + std::exp(-a / bb));
+      const double x = (s - a) / bb;
+      if (x > 36.7) {
+        rho[0] = s - a - c;
+        rho[1] = 1.0;
+        rho[2] = 0.0;
+      } else {
+        const double e_x = std::exp(x);
+        rho[0] = bb * std::log(1.0 + e_x) - c;
+        rho[1] = std::max(std::numeric_limits<double>::min(), e_x / (1.0 + e_x));
+        rho[2] = 0.5 / (bb * (1.0 + std::cosh(x)));
+      }
+      break;
+    }
     case ORACLE_LOSS_HUBER: {
       const double b = a * a;
       if (s > b) {
@@ -654,7 +705,7 @@ static bool EvaluateResidualBlock(const Prepared& P, int64_t i,
   }
   double rho[3];
   Loss(p->rb_loss_kind[i], p->rb_loss_a[i], p->rb_loss_scaled[i], p->rb_loss_scale[i],
-       squared_norm, rho);
+       squared_norm, rho, p->rb_loss_b ? p->rb_loss_b[i] : 0.0);
   *cost = 0.5 * rho[0];
   Corrector correct(squared_norm, rho);
   if (jacobians)
@@ -950,6 +1001,11 @@ extern "C" void oracle_quaternion_rotate_point(const double q[4], const double p
 extern "C" void oracle_loss(int kind, double a, int scaled, double scale, double s,
                             double rho[3]) {
   Loss(kind, a, scaled, scale, s, rho);
+}
+
+extern "C" void oracle_loss_ab(int kind, double a, double b, int scaled, double scale, double s,
+                               double rho[3]) {
+  Loss(kind, a, scaled, scale, s, rho, b);
 }
 
 extern "C" void oracle_corrector(double sq_norm, const double rho[3], int num_rows,

@@ -20,6 +20,12 @@ P_i64 = C.POINTER(C.c_int64)
 P_f64 = C.POINTER(C.c_double)
 
 
+# oracle.h kinds/losses the GPU side reaches through user functor kinds
+BUNDLER_RESIDUAL_2_9_3 = 5
+LOSS_SOFT_L_ONE = 10
+LOSS_TOLERANT = 11
+
+
 class oracle_program(C.Structure):
     _fields_ = [("num_parameter_blocks", C.c_int64), ("pb_size", P_i32),
                 ("pb_tangent_size", P_i32), ("pb_constant", P_i32),
@@ -28,7 +34,8 @@ class oracle_program(C.Structure):
                 ("rb_loss_kind", P_i32), ("rb_loss_a", P_f64), ("rb_loss_scale", P_f64),
                 ("rb_loss_scaled", P_i32), ("rb_param_begin", P_i64), ("rb_params", P_i32),
                 ("rb_data_begin", P_i64), ("rb_data", P_f64), ("jacobian_format", C.c_int32),
-                ("num_eliminate_blocks", C.c_int32), ("apply_loss_function", C.c_int32)]
+                ("num_eliminate_blocks", C.c_int32), ("apply_loss_function", C.c_int32),
+                ("rb_loss_b", P_f64)]
 
 
 class oracle_sizes(C.Structure):
@@ -68,6 +75,8 @@ def lib():
         L.oracle_angle_axis_rotate_point.argtypes = [P_f64, P_f64, P_f64]
         L.oracle_quaternion_rotate_point.argtypes = [P_f64, P_f64, P_f64]
         L.oracle_loss.argtypes = [C.c_int, C.c_double, C.c_int, C.c_double, C.c_double, P_f64]
+        L.oracle_loss_ab.argtypes = [C.c_int, C.c_double, C.c_double, C.c_int, C.c_double,
+                                     C.c_double, P_f64]
         L.oracle_corrector.argtypes = [C.c_double, P_f64, C.c_int, C.c_int, P_f64, P_f64]
         L.oracle_autodiff.argtypes = [C.c_int, P_f64, C.POINTER(P_f64), P_f64, C.POINTER(P_f64)]
         L.oracle_jet_op.argtypes = [C.c_int, P_f64, P_f64, P_f64, P_f64]
@@ -86,7 +95,7 @@ class OracleProgram:
     def __init__(self, pb_size, pb_tangent, pb_constant, pb_plus_jacobian, plus_jacobians,
                  rb_kind, rb_loss_kind, rb_loss_a, rb_loss_scale, rb_loss_scaled, rb_param_begin,
                  rb_params, rb_data_begin, rb_data, jacobian_format, num_eliminate_blocks,
-                 apply_loss_function=1):
+                 apply_loss_function=1, rb_loss_b=None):
         arr = lambda x, t: np.ascontiguousarray(np.asarray(x), t)
         self.a = dict(pb_size=arr(pb_size, np.int32), pb_tangent=arr(pb_tangent, np.int32),
                       pb_constant=arr(pb_constant, np.int32),
@@ -95,7 +104,8 @@ class OracleProgram:
                       la=arr(rb_loss_a, np.float64), ls=arr(rb_loss_scale, np.float64),
                       lsd=arr(rb_loss_scaled, np.int32), pbeg=arr(rb_param_begin, np.int64),
                       params=arr(rb_params, np.int32), dbeg=arr(rb_data_begin, np.int64),
-                      data=arr(rb_data, np.float64))
+                      data=arr(rb_data, np.float64),
+                      lb=None if rb_loss_b is None else arr(rb_loss_b, np.float64))
         a = self.a
         self.s = oracle_program(len(a["pb_size"]), _p(a["pb_size"], C.c_int32),
                                 _p(a["pb_tangent"], C.c_int32), _p(a["pb_constant"], C.c_int32),
@@ -105,10 +115,13 @@ class OracleProgram:
                                 _p(a["lsd"], C.c_int32), _p(a["pbeg"], C.c_int64),
                                 _p(a["params"], C.c_int32), _p(a["dbeg"], C.c_int64),
                                 _p(a["data"], C.c_double), int(jacobian_format),
-                                int(num_eliminate_blocks), int(apply_loss_function))
+                                int(num_eliminate_blocks), int(apply_loss_function),
+                                _p(a["lb"], C.c_double))
 
     @classmethod
-    def from_program(cls, prog, apply_loss_function=True):
+    def from_program(cls, prog, apply_loss_function=True, kind_map=None, loss_map=None):
+        """kind_map: functor kind -> oracle kind (user functor kinds);
+        loss_map: Loss -> (oracle loss kind, a, b) for user losses."""
         # The reference's form: every manifold as its explicit plus-Jacobian
         # (Program.with_explicit_manifolds, at the Program's state).
         if getattr(prog, "pb_manifold", None) is not None and np.any(prog.pb_manifold):
@@ -119,13 +132,16 @@ class OracleProgram:
         la = np.ones(nrb)
         ls = np.ones(nrb)
         lsd = np.zeros(nrb, np.int32)
+        lb = np.zeros(nrb)
         nb = np.zeros(nrb, np.int64)
         nd = np.zeros(nrb, np.int64)
         for g in prog.groups:
             idx = g.index if g.index is not None else np.arange(g.first, g.first + g.n)
-            kind[idx] = g.kind
+            kind[idx] = (kind_map or {}).get(g.kind, g.kind)
             lk[idx] = g.loss.kind
             la[idx] = g.loss.a
+            if loss_map is not None and g.loss.kind == 3:  # LOSS_USER
+                lk[idx], la[idx], lb[idx] = loss_map(g.loss)
             ls[idx] = g.loss.scale
             lsd[idx] = int(g.loss.scaled)
             nb[idx] = g.ids.shape[1]
@@ -144,7 +160,7 @@ class OracleProgram:
         return cls(prog.pb_size, prog.pb_tangent, prog.pb_constant, prog.pb_plus_jacobian,
                    prog.plus_jacobians if prog.plus_jacobians.size else np.zeros(1), kind, lk, la,
                    ls, lsd, pbeg, params, dbeg, data, fmt, prog.num_eliminate_blocks,
-                   int(apply_loss_function))
+                   int(apply_loss_function), lb)
 
     def sizes(self):
         s = oracle_sizes()
@@ -235,9 +251,9 @@ def quaternion_rotate_point(q, pt):
     return out
 
 
-def loss(kind, a, s, scaled=False, scale=1.0):
+def loss(kind, a, s, scaled=False, scale=1.0, b=0.0):
     rho = np.empty(3)
-    lib().oracle_loss(kind, a, int(scaled), scale, s, _p(rho, C.c_double))
+    lib().oracle_loss_ab(kind, a, b, int(scaled), scale, s, _p(rho, C.c_double))
     return rho
 
 

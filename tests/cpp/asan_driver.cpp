@@ -266,6 +266,20 @@ static void RunFormat(const Bal& b, bool crs) {
     EXPECT(IsApprox(o.r, o1.r, 1e-13));
     EXPECT(IsApprox(o.g, o1.g, 1e-13));
     EXPECT(IsApprox(o.J, o1.J, 1e-13));
+    // Program::Plus in place (out == state, program.cc:121-149): bit-equal to
+    // separate buffers; on the multi-device evaluator cameras are held by
+    // several shards (MultiPlus gathers every input before writing).
+    {
+      std::vector<double> delta(sz.num_effective_parameters), sep(b.state.size());
+      for (size_t k = 0; k < delta.size(); ++k) delta[k] = 1e-3 * std::sin(0.37 * (double)k);
+      std::vector<double> x = b.state;
+      EXPECT(cse_plus(ev, b.state.data(), delta.data(), sep.data()) == CSE_OK);
+      EXPECT(cse_plus(ev, x.data(), delta.data(), x.data()) == CSE_OK);
+      EXPECT(x == sep);
+      bool plain = true;
+      for (size_t k = 0; k < x.size(); ++k) plain = plain && sep[k] == b.state[k] + delta[k];
+      EXPECT(plain);
+    }
     int32_t n = 0;
     EXPECT(cse_shard_info(ev, &n, nullptr, nullptr) == CSE_OK && n == (multi ? 3 : 1));
     cse_info info;

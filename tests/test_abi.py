@@ -43,9 +43,9 @@ def test_abi_version_and_build_info():
 def test_struct_layouts_match_header():
     """ctypes mirrors of the descriptor structs have the C sizes."""
     from ceres_amd import _cse
-    assert ctypes.sizeof(_cse.cse_loss) == 24
+    assert ctypes.sizeof(_cse.cse_loss) == 88  # ABI 4: 64 bytes of user loss object
     assert ctypes.sizeof(_cse.cse_parameter_block) == 40
-    assert ctypes.sizeof(_cse.cse_residual_group) == 72
+    assert ctypes.sizeof(_cse.cse_residual_group) == 136
     assert ctypes.sizeof(_cse.cse_options) == 40
 
 

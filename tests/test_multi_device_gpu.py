@@ -308,3 +308,28 @@ def test_configs4_problem_13682_per_rank_shards(gpu, problem_13682, fmt):
     assert_parity((True, cost_ng, R_ng, None, J_ng), (ref[0], ref[1], ref[2], None, ref[4]),
                   ("configs[4] per-rank shards, no gradient", fmt), report=rep_ng)
     print(f"configs[4] (8 per-rank shards) {fmt} Huber, residual+Jacobian kernel:", rep_ng)
+
+
+@pytest.mark.parametrize("nshards", [1, 3])
+def test_plus_in_place_on_a_multi_device_evaluator(gpu, nshards):
+    """cse_plus with out == state (Program::Plus(x, delta, x), program.cc:
+    121-149) on cse_create_multi: every camera is held by several shards,
+    each shard gathers its inputs before any writes, so the in-place result
+    is bit-equal to separate buffers (ADVICE r4 #1)."""
+    prog = bal.synthetic_program((20, 3001, 21113), loss=ca.Loss.huber(1.0), seed=35)
+    rng = np.random.default_rng(9)
+    delta = rng.normal(scale=1e-3, size=prog.num_effective_parameters)
+    ev = ca.Evaluator(prog, devices=[0] * nshards)
+    try:
+        first, _ = ev.shard_info()
+        if nshards > 1:  # cameras shared by several shards
+            cams = [set(prog.groups[0].ids[first[k]:first[k + 1], 0]) for k in range(nshards)]
+            assert cams[0] & cams[1]
+        separate = ev.plus(prog.state, delta)
+        x = prog.state.copy()
+        same = ev.plus(x, delta, out=x)
+        assert same is x
+    finally:
+        ev.close()
+    assert np.array_equal(x, separate)
+    assert np.array_equal(separate, prog.state + delta)  # no manifold: x + delta

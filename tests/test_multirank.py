@@ -27,7 +27,27 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, fmt, q, held=()):
+def _skewed(seed=21, C=12, P=700):
+    """A BAL-shaped problem with ragged point buckets: most points seen by 2-4
+    cameras, a few by many more (a rank's cut then lands far from its
+    balanced target)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
+    from ceres_amd import bal
+    cams, pts, ci, pi, obs = bal.synthetic(C, P, 3 * P, seed=seed)
+    rng = np.random.default_rng(seed)
+    per = rng.integers(2, 5, P)
+    per[rng.choice(P, 6, replace=False)] = C  # heavy points: every camera
+    ci2, pi2, obs2 = [], [], []
+    for p in range(P):
+        cs = rng.choice(C, per[p], replace=False)
+        ci2.extend(cs)
+        pi2.extend([p] * len(cs))
+        obs2.extend(rng.normal(scale=50.0, size=(len(cs), 2)))
+    return cams, pts, np.array(ci2, np.int32), np.array(pi2, np.int32), np.array(obs2)
+
+
+def _worker(rank, world, port, fmt, q, held=(), skewed=False):
     import sys
     for p in (os.path.join(REPO, "ceres-solver-cuda_amd"), os.path.join(REPO, "oracle"),
               os.path.join(REPO, "tests")):
@@ -41,10 +61,23 @@ def _worker(rank, world, port, fmt, q, held=()):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         C, P, Obs = 12, 700, 2600
-        cams, pts, ci, pi, obs = bal.synthetic(C, P, Obs, seed=21)
+        if skewed:
+            cams, pts, ci, pi, obs = _skewed()
+            Obs = len(ci)
+        else:
+            cams, pts, ci, pi, obs = bal.synthetic(C, P, Obs, seed=21)
         loss = ca.Loss.huber(1.0)
         prog, sh = shard.shard_program(cams, pts, ci, pi, obs, rank, world, loss=loss, format=fmt,
                                        constant_cameras=held)
+        # The rank's blocks, points and strips are the point-bucket cut's
+        # (what bench.py --gpus N reports as blocks_rank0 / strip_rank0).
+        pc, bc = shard.point_bucket_cuts(pi, P, world)
+        assert sh.blocks == (bc[rank], bc[rank + 1]) and sh.points == (pc[rank], pc[rank + 1])
+        assert sh.residual_strip == (2 * bc[rank], 2 * bc[rank + 1])
+        if fmt == "block_sparse" and not held:
+            assert [g for _, g, _ in sh.jacobian_strips()] == [6 * bc[rank], 6 * Obs + 18 * bc[rank]]
+        elif fmt == "compressed_row":
+            assert sh.jacobian_strips() == [(0, 24 * bc[rank], 24 * (bc[rank + 1] - bc[rank]))]
         cs = prog.constant_state if prog.constant_state.size else None
         ok, cost, r, g, j = O.OracleProgram.from_program(prog).evaluate(prog.state, cs, num_threads=2)
         assert ok
@@ -71,7 +104,9 @@ def _worker(rank, world, port, fmt, q, held=()):
             G = np.concatenate([p[3] for p in parts] + [gcam.numpy()])
             assert is_approx(G, gf, 1e-13)
             sizes = [p[0].blocks[1] - p[0].blocks[0] for p in parts]
-            assert sum(sizes) == Obs and max(sizes) - min(sizes) <= 2 * (Obs // P + 1)
+            assert sum(sizes) == Obs and min(sizes) > 0
+            if not skewed:
+                assert max(sizes) - min(sizes) <= 2 * (Obs // P + 1)
         q.put((rank, "ok"))
     except Exception as e:  # report to the parent
         q.put((rank, repr(e)))
@@ -80,15 +115,12 @@ def _worker(rank, world, port, fmt, q, held=()):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("fmt,held", [("block_sparse", ()), ("compressed_row", ()),
-                                      ("block_sparse", (0, 5))])
-def test_sharded_evaluation_matches_unsharded(world, fmt, held):
-    # held: cameras held constant (their blocks have no F cell; Shard.f_cells)
+def _run(world, fmt, held=(), skewed=False):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, q, held)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fmt, q, held, skewed))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -96,6 +128,22 @@ def test_sharded_evaluation_matches_unsharded(world, fmt, held):
     results = dict(q.get() for _ in range(world))
     assert all(v == "ok" for v in results.values()), results
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("fmt,held", [("block_sparse", ()), ("compressed_row", ()),
+                                      ("block_sparse", (0, 5))])
+def test_sharded_evaluation_matches_unsharded(world, fmt, held):
+    # held: cameras held constant (their blocks have no F cell; Shard.f_cells)
+    _run(world, fmt, held)
+
+
+@pytest.mark.parametrize("fmt", ["block_sparse", "compressed_row"])
+def test_eight_ranks_ragged_cuts(fmt):
+    """BASELINE.json configs[4]'s rank count (8) over gloo, on a problem with
+    ragged point buckets: the assembled strips equal the unsharded
+    evaluation bit for bit and every rank's blocks / strips are the cut's."""
+    _run(8, fmt, skewed=True)
 
 
 def test_point_bucket_cuts_properties():
