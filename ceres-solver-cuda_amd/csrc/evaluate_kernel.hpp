@@ -260,52 +260,37 @@ __device__ __forceinline__ void GatherCoop(const GroupArgs& a, int64_t i, int2 i
 // 16 B at lds + 16 * p, so the pieces land in block order without passing
 // through VGPRs.  The once-read streams (ids, observations, points) load
 // non-temporally (-1.3 %, profiles/r02).
-// Tuning build: kStride (doubles, 0 = PackedRowDoubles) is the table's row
-// stride, which the host must have repacked with; kOwn: each lane fetches
-// its own block's pieces (no bpermute, 64 rows per instruction) into
-// piece-major LDS.
-template <class K, int kStride = 0, bool kOwn = false>
+template <class K>
 __device__ __forceinline__ void GatherCoopDma(const GroupArgs& a, int64_t i, int2 id,
                                               AffineInputs<K>* in, double* lds, int lane) {
   using Tr = KindTraits<K>;
   constexpr int X0 = Tr::X0;
   constexpr int X0p = (X0 + 1) & ~1;  // doubles per block in the packed table
   constexpr int kPieces = X0p / 2;    // 16-byte pieces per block
-  constexpr int kRow = kStride ? kStride : PackedRowDoubles(X0);
+  constexpr int kRow = PackedRowDoubles(X0);
   const int cid_own = id.x - a.packed0_lo;
 #pragma unroll
   for (int k = 0; k < kPieces; ++k) {
-    if constexpr (kOwn) {
-      const double* src = a.packed0 + (int64_t)kRow * cid_own + 2 * k;
-      __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
-    } else {
-      const int p = k * kWave + lane;
-      const int t = p / kPieces, q = p - t * kPieces;
-      const int cid = __shfl(cid_own, t, kWave);
-      const double* src = a.packed0 + (int64_t)kRow * cid + 2 * q;
-      __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
-    }
+    const int p = k * kWave + lane;
+    const int t = p / kPieces, q = p - t * kPieces;
+    const int cid = __shfl(cid_own, t, kWave);
+    const double* src = a.packed0 + (int64_t)kRow * cid + 2 * q;
+    __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
   }
   GatherDataAndSlot1<K, true>(a, i, id, in);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  if constexpr (kOwn) {
 #pragma unroll
-    for (int k = 0; k < X0; ++k) in->x0[k] = lds[2 * kWave * (k / 2) + 2 * lane + (k & 1)];
-  } else {
-#pragma unroll
-    for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
-    if constexpr (X0 < X0p) in->x0pad = lds[lane * X0p + X0];
-  }
+  for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
+  if constexpr (X0 < X0p) in->x0pad = lds[lane * X0p + X0];
   __builtin_amdgcn_wave_barrier();
   in->id0 = id.x;
   in->id1 = id.y;
 }
 
-// Tuning build: the observation load issued before the ids are waited for
-// (kEarlyObs), and optionally slot 0 straight into registers from the
-// repacked table, 16 bytes a load (kRegGather).
-template <class K, bool kReg>
+// The same with the observation load issued before the ids are waited for
+// (the residual-only and cost-only kernels).
+template <class K>
 __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 id,
                                             AffineInputs<K>* in, double* lds, int lane) {
   using Tr = KindTraits<K>;
@@ -316,23 +301,13 @@ __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 
   const double obs_x = __builtin_nontemporal_load(a.data + 2 * i);
   const double obs_y = __builtin_nontemporal_load(a.data + 2 * i + 1);
   const int cid_own = id.x - a.packed0_lo;
-  if constexpr (kReg) {
-    const double2* src =
-        reinterpret_cast<const double2*>(a.packed0 + (int64_t)PackedRowDoubles(X0) * cid_own);
-    double2 v[kPieces];
 #pragma unroll
-    for (int k = 0; k < kPieces; ++k) v[k] = src[k];
-#pragma unroll
-    for (int k = 0; k < X0; ++k) in->x0[k] = (k & 1) ? v[k / 2].y : v[k / 2].x;
-  } else {
-#pragma unroll
-    for (int k = 0; k < kPieces; ++k) {
-      const int p = k * kWave + lane;
-      const int t = p / kPieces, q = p - t * kPieces;
-      const int cid = __shfl(cid_own, t, kWave);
-      const double* src = a.packed0 + (int64_t)PackedRowDoubles(X0) * cid + 2 * q;
-      __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
-    }
+  for (int k = 0; k < kPieces; ++k) {
+    const int p = k * kWave + lane;
+    const int t = p / kPieces, q = p - t * kPieces;
+    const int cid = __shfl(cid_own, t, kWave);
+    const double* src = a.packed0 + (int64_t)PackedRowDoubles(X0) * cid + 2 * q;
+    __builtin_amdgcn_global_load_lds(src, lds + 2 * kWave * k, 16, 0, 0);
   }
   if constexpr (S1 > 0) {
     const double* p1 = a.state + a.state_base[1] + (int64_t)S1 * id.y;
@@ -341,13 +316,11 @@ __device__ __forceinline__ void GatherEarly(const GroupArgs& a, int64_t i, int2 
   }
   in->d[0] = obs_x;
   in->d[1] = obs_y;
-  if constexpr (!kReg) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
-    __builtin_amdgcn_wave_barrier();
-  }
+  for (int k = 0; k < X0; ++k) in->x0[k] = lds[lane * X0p + k];
+  __builtin_amdgcn_wave_barrier();
   in->id0 = id.x;
   in->id1 = id.y;
 }
@@ -440,13 +413,6 @@ struct FusedGrad {
   }
 };
 
-// The points-only fused kernel writes the slot-1 copy for
-// CameraGradientKernel (GroupArgs::ppad): each point once per wave, by the
-// last lane of its run, from the values the wave loaded anyway.  Off
-// (CSE_POINT_COPY 0): measured neutral on problem-13682 (2.128 vs 2.133 ms
-// per gradient evaluation, profiles/round4/r4g/ab_grad) -- the camera
-// kernel's 24-byte point gathers already cost one sector request each, so a
-// sector-aligned copy saves no requests; -DCSE_POINT_COPY=1 builds it.
 // Waves per CU of the one-wave Jacobian kernels, capped through their LDS
 // footprint (doubles a lane; 0 = no cap).  BSM: 20 (10 KiB, 16 waves per
 // CU).  With the by-hand Snavely functor the kernel needs only 92 VGPRs and
@@ -455,48 +421,27 @@ struct FusedGrad {
 // interleave.  With the tail storing F, E, residuals: 1.400 ms at 12 waves
 // per CU, 1.44 at 13-14, 1.50 at 16, 1.525 at 17 (profiles/round4/r4occ,
 // r4occ2, r4s7; the Jet kernel 1.427 at 16).  Storing E first (E, F,
-// residuals; CSE_STORE_ORDER 2): 1.346-1.354 at 12, 1.326-1.336 at 14,
+// residuals; ShippedTune's order 2): 1.346-1.354 at 12, 1.326-1.336 at 14,
 // 1.314-1.321 at 16 (r4ord2), and 16 ahead of 15 and 17 on another box
 // (r4ord3).  CRS (one output stream) is fastest uncapped (20 waves per CU).
-#ifndef CSE_STAGE_MIN_LANE
-#define CSE_STAGE_MIN_LANE 20
-#endif
-// A/B builds: the Jacobian kernels' chunks in XCD-contiguous ranges (1).
-#ifndef CSE_XCD_MAP
-#define CSE_XCD_MAP 0
-#endif
-#ifndef CSE_STAGE_MIN_LANE_CRS
-#define CSE_STAGE_MIN_LANE_CRS 0
-#endif
+constexpr int kStageMinLane = 20;
+constexpr int kStageMinLaneCrs = 0;
 // The fused gradient's points kernel (94 VGPRs by hand): capped at 16 waves
 // per CU like the Jet kernel's register bound (uncapped, 17, the gradient
 // evaluation took 2.157-2.163 ms against 2.119-2.124 for the Jet build,
 // profiles/round4/r4grad2; capped at 16, 2.126-2.133 against 2.124-2.131,
 // r4s7).
-#ifndef CSE_STAGE_MIN_LANE_FP
-#define CSE_STAGE_MIN_LANE_FP 20
-#endif
-// The held-camera tail's E cells before its F window (1, shipped: held
+constexpr int kStageMinLaneFp = 20;
+// The held-camera tail stores its E cells before its F window (held
 // evaluation 1.435-1.439 against 1.462-1.471 ms with E after F, the unheld
-// evaluation 1.425-1.427 on that box; profiles/round4/r4held5) or after (0).
-#ifndef CSE_C0_E_FIRST
-#define CSE_C0_E_FIRST 1
-#endif
+// evaluation 1.425-1.427 on that box; profiles/round4/r4held5).
 // The held-camera BSM kernel likewise: 1.444-1.447 ms capped at 12 against
 // 1.51-1.54 uncapped (16 per CU; profiles/round4/r4s8).
 // The residual-only and cost-only kernels (8 waves per SIMD, 60 VGPRs) are
 // fastest uncapped: capped at 24 waves per CU alike, at 16 7-15 % slower
 // (profiles/round4/r4res).
-#ifndef CSE_STAGE_MIN_LANE_RES
-#define CSE_STAGE_MIN_LANE_RES 0
-#endif
-#ifndef CSE_STAGE_MIN_LANE_C0
-#define CSE_STAGE_MIN_LANE_C0 26
-#endif
-
-#ifndef CSE_POINT_COPY
-#define CSE_POINT_COPY 0
-#endif
+constexpr int kStageMinLaneRes = 0;
+constexpr int kStageMinLaneC0 = 26;
 
 // Can the wave take the back-to-back store tail?  Full chunk, 16-byte
 // pieces that tile every segment exactly, 16-byte-aligned destinations.
@@ -615,115 +560,46 @@ __device__ __forceinline__ void SegmentStoresMasked(double* b0, double* b1, cons
   }
 }
 
-// Compile-time knobs of the affine kernel.  The product instantiates only
-// ShippedTune; other settings exist in the tuning build (-DCSE_TUNING,
-// tools/), never in libcse.so.
-//   kPrio   s_setprio around the memory phases: 0 none; 1 priority 2 from
-//           the Jacobian staging to the end (the store tail); 2 also during
-//           the gather issue, priority 0 while computing.
-//   kLdsE   stage the slot-1 (E) cells through LDS with the F cells (true),
-//           or store each lane's E cell straight from registers, 48 B per
-//           lane (false: 2/3 of the LDS, 4 workgroups per CU).
-//   kTwoRound  stage the F cells, read them back, then stage the E cells in
-//           the same LDS (9 KiB a wave instead of 12: 4 workgroups per CU).
-//   kMinLane  at least this many doubles of LDS per lane (an occupancy
-//           limit: 28 -> 56 KiB a workgroup, 2 workgroups per CU).
-//   kAlign  the store windows' alignment unit (SectorHeadPieces), bytes.
+// Compile-time settings of the affine kernel (the four the product ships,
+// below).  Measured alternatives of rounds 2-5 -- wave priorities, E cells
+// from registers, one-round staging, LDS occupancy caps, 128-byte windows,
+// early observation loads, register gathers, other table strides, own-row
+// DMA, store cache policies, XCD-contiguous chunks, scalar id loads --
+// were slower and are not in the tree (git history before
+// round 6).
 //   kOrder  the store tail's order: 0 F, E, residuals; 1 residuals, E, F;
 //           2 E, F, residuals.
-//   kEarlyObs  issue the observation load with the ids load, before the
-//           ids are waited for (the camera and point loads depend on them).
-//   kRegGather slot 0 loaded lane by lane from the repacked table into
-//           registers (no bpermute, no LDS round trip) instead of LDS-DMA.
-//   kDiag   diagnostic (wrong results by design): 1 replaces the functor by
-//           a few additions of its inputs -- the memory path's floor; 2
-//           reads every lane's slot-0 block from the first table row (a
-//           broadcast, no gather) -- the camera gather's cost; 3 both; 4
-//           no Jacobian stores (residuals and partials only); 5 no E stores.
-//   kCamStride the repacked slot-0 table's row stride in doubles (0:
-//           PackedRowDoubles; the host repacks at $CSE_TUNE_CAMSTRIDE).
-//   kDmaOwn  LDS-DMA of each lane's own row (GatherCoopDma kOwn).
 //   kNoContrib  fused gradient without the slot-0 contributions (the slot-0
 //           sums come from CameraGradientKernel instead).
-//   kEPol, kRPol  cache policy (StoreNt16 kPol) of the E-cell and residual
-//           stores (the F cells keep nt sc1).
-template <int kPrio_ = 0, bool kLdsE_ = true, bool kTwoRound_ = false, int kMinLane_ = 0,
-          int kAlign_ = 64, int kOrder_ = 0, bool kEarlyObs_ = false, bool kRegGather_ = false,
-          int kDiag_ = 0, int kCamStride_ = 0, bool kDmaOwn_ = false, bool kNoContrib_ = false,
-          int kEPol_ = 0, int kRPol_ = 0, int kFPol_ = 0, bool kConst0_ = false,
-          bool kXcdMap_ = false, bool kScalarIds_ = false, bool kProbe_ = false>
+//   kConst0 the group has constant slot-0 blocks (BSM: their F cells are
+//           packed, fbase).
+template <int kOrder_, bool kNoContrib_ = false, bool kConst0_ = false>
 struct Tune {
-  static constexpr int kPrio = kPrio_;
-  static constexpr bool kLdsE = kLdsE_;
-  static constexpr bool kTwoRound = kTwoRound_;
-  static constexpr int kMinLane = kMinLane_;
-  static constexpr int kAlign = kAlign_;
   static constexpr int kOrder = kOrder_;
-  static constexpr bool kEarlyObs = kEarlyObs_;
-  static constexpr bool kRegGather = kRegGather_;
-  static constexpr int kDiag = kDiag_;
-  static constexpr int kCamStride = kCamStride_;
-  static constexpr bool kDmaOwn = kDmaOwn_;
   static constexpr bool kNoContrib = kNoContrib_;
-  static constexpr int kEPol = kEPol_;  // StoreNt16 policy of the E-cell stores
-  static constexpr int kRPol = kRPol_;  // and of the residual stores
-  static constexpr int kFPol = kFPol_;  // and of the F-cell stores
-  static constexpr bool kConst0 = kConst0_;  // constant slot-0 blocks (BSM)
-  // Workgroups dispatched round-robin over the 8 XCDs get contiguous chunk
-  // ranges per XCD (workgroup b -> XCD b % 8, remapped to a bijection).
-  static constexpr bool kXcdMap = kXcdMap_;
-  // Full chunks read their 64 slot-0 ids through the scalar cache (s_load,
-  // then v_writelane), so the camera gather's addresses do not wait on a
-  // vector load queued behind other waves' stores (tuning build).
-  static constexpr bool kScalarIds = kScalarIds_;
-  // Per-wave phase stamps (s_memtime) into a.probe[chunk][8]: ids arrived,
-  // gather arrived, outputs ready, stores issued (tuning build).
-  static constexpr bool kProbe = kProbe_;
+  static constexpr bool kConst0 = kConst0_;
 };
 
-// The logical workgroup of dispatch index b when each of the 8 XCDs is to
-// take one contiguous range of the grid (round-robin dispatch: b -> XCD
-// b % 8): XCD x owns [x*q + min(x, r), ...) of q + (x < r) workgroups.
-__device__ __forceinline__ int64_t XcdContiguous(int64_t b, int64_t nwg) {
-  const int64_t x = b & 7, k = b >> 3, q = nwg >> 3, r = nwg & 7;
-  return x * q + (x < r ? x : r) + k;
-}
 // Shipped: no priority changes (kPrio 2 was 1.5-2 % faster with the library
 // sincos and divisions, profiles/round2/s1, s3c, and 2 % slower once the
 // functor's FP64 work shrank, s3d); two-round E/F staging (9 KiB of LDS a
-// wave), which with the kernel held to 128 VGPRs (EvaluateAffineChunksTwoRound)
-// gives 4 waves per SIMD instead of 3.  That was neutral with the heavier
-// functor (s3i, s3j) and is 2.5 % faster with the series rotation (s4n).
-// The store tail's segment order: 0 = F, E, residuals; 1 = residuals, E, F;
-// 2 = E, F, residuals (shipped: with the BSM kernel at 12 waves per CU,
-// 1.369-1.373 ms against 1.397-1.398 for 0 and 1.369-1.377 for 1; CRS
-// neutral; profiles/round4/r4ord).
-#ifndef CSE_STORE_ORDER
-#define CSE_STORE_ORDER 2
-#endif
-using ShippedTune = Tune<0, true, true, 0, 64, CSE_STORE_ORDER>;
+// wave), which with the kernel held to 128 VGPRs gives 4 waves per SIMD
+// instead of 3.  That was neutral with the heavier functor (s3i, s3j) and is
+// 2.5 % faster with the series rotation (s4n).
+// The store tail's segment order E, F, residuals (2): with the BSM kernel at
+// 12 waves per CU, 1.369-1.373 ms against 1.397-1.398 for 0 and 1.369-1.377
+// for 1; CRS neutral; profiles/round4/r4ord.
+using ShippedTune = Tune<2>;
 // The fused gradient's points-only form (CameraGradientKernel adds slot 0).
-// Its store order (as CSE_STORE_ORDER): residuals, E, F (1) -- gradient
-// evaluation 1.965-1.970 ms against 2.017-2.026 for F, E, residuals (0) and
-// 1.976-1.978 for E, F, residuals (2), same box (profiles/round4/r4fpord).
-#ifndef CSE_FP_STORE_ORDER
-#define CSE_FP_STORE_ORDER 1
-#endif
-using PointsOnlyTune = Tune<0, true, true, 0, 64, CSE_FP_STORE_ORDER, false, false, 0, 0, false, true>;
+// Its store order: residuals, E, F (1) -- gradient evaluation 1.965-1.970
+// ms against 2.017-2.026 for F, E, residuals (0) and 1.976-1.978 for E, F,
+// residuals (2), same box (profiles/round4/r4fpord).
+using PointsOnlyTune = Tune<1, true>;
 // The same for groups with constant slot-0 blocks (a held camera): a wave
 // with one takes the slow tail, its F cells packed from fbase[c]; waves
 // without take the fast tail from fbase[c].
-using ShippedTuneC0 = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, false, 0, 0, 0, true>;
-using PointsOnlyTuneC0 = Tune<0, true, true, 0, 64, 0, false, false, 0, 0, false, true, 0, 0, 0, true>;
-
-// The settings the product (libcse.so) may instantiate; anything else exists
-// only in the tuning build (-DCSE_TUNING: tools/ A/B runs), where the
-// diagnostic kDiag settings deliberately write wrong values.
-template <class T>
-constexpr bool kProductTune = std::is_same<T, ShippedTune>::value ||
-                              std::is_same<T, PointsOnlyTune>::value ||
-                              std::is_same<T, ShippedTuneC0>::value ||
-                              std::is_same<T, PointsOnlyTuneC0>::value;
+using ShippedTuneC0 = Tune<0, false, true>;
+using PointsOnlyTuneC0 = Tune<0, true, true>;
 
 // Does the shipped BSM Jacobian kernel of kind K stage in two rounds (and so
 // fit 4 workgroups per CU)?
@@ -747,17 +623,13 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, N = S0 + S1;
   static_assert(!MayLeaveOutputs<K>::value, "affine kernels: functors that assign every output");
-#ifndef CSE_TUNING
-  static_assert(kProductTune<T>, "libcse.so instantiates the shipped settings only (tuning build: -DCSE_TUNING)");
-#endif
-  constexpr bool kLdsE = T::kLdsE || kCrs || !kJac;
-  constexpr bool kTwo = T::kTwoRound && kJac && !kCrs && kLdsE && S1 > 0;
-  // CRS rows staged in two halves of the wave (lanes [0, 32), then [32, 64)).
-  constexpr bool kTwoCrs = T::kTwoRound && kJac && kCrs;
-  constexpr int kA = T::kAlign;
-  constexpr int kOutLane = kJac ? (kCrs ? (kTwoCrs ? (NR * N + 1) / 2 : NR * N)
-                                        : kTwo ? NR * (S0 > S1 ? S0 : S1)
-                                               : kLdsE ? NR * (S0 + S1) : NR * S0)
+  // BSM: the F cells staged and read back, then the E cells in the same LDS
+  // (two rounds); CRS rows staged in two halves of the wave (lanes [0, 32),
+  // then [32, 64)).
+  constexpr bool kTwo = kJac && !kCrs && S1 > 0;
+  constexpr bool kTwoCrs = kJac && kCrs;
+  constexpr int kOutLane = kJac ? (kCrs ? (NR * N + 1) / 2
+                                        : kTwo ? NR * (S0 > S1 ? S0 : S1) : NR * (S0 + S1))
                                 : 1;
   constexpr int kCoopLane = kCoop == 2 ? ((Tr::X0 + 1) & ~1) : Tr::X0;
   // StageAndStore's footprint (ragged chunks): whole rows (CRS) or one
@@ -768,27 +640,24 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   constexpr int kOutLane1 = kContribLane > kOutLane ? kContribLane : kOutLane;
   constexpr int kStageLane0 = kCoopLane > kOutLane1 ? kCoopLane : kOutLane1;
   constexpr int kStageLane1 = kSlowLane > kStageLane0 ? kSlowLane : kStageLane0;
-  // The LDS cap on waves per CU (CSE_STAGE_MIN_LANE, above), for the
+  // The LDS cap on waves per CU (kStageMinLane, above), for the
   // by-hand Snavely kernels only (the Jet-based quaternion kernel is
   // register-bound at 16 waves per CU and slower capped: 1.516 vs 1.38 ms,
   // r4s9); the fused gradient's points kernel measured neutral to it (r4s7).
-  constexpr bool kByHand = std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0;
-  constexpr int kPadLane = !kJac ? (std::is_same<K, SnavelyKind>::value ? CSE_STAGE_MIN_LANE_RES : 0)
+  constexpr bool kByHand = std::is_same<K, SnavelyKind>::value;
+  constexpr int kPadLane = !kJac ? (std::is_same<K, SnavelyKind>::value ? kStageMinLaneRes : 0)
                           : kWPB != 1 || !kByHand ? 0
-                          : T::kConst0 ? (kGradF || kCrs ? 0 : CSE_STAGE_MIN_LANE_C0)
-                          : kGradF ? CSE_STAGE_MIN_LANE_FP
-                          : kCrs ? CSE_STAGE_MIN_LANE_CRS : CSE_STAGE_MIN_LANE;
-  constexpr int kMinLane = kPadLane > T::kMinLane ? kPadLane : T::kMinLane;
-  constexpr int kStageLane = kMinLane > kStageLane1 ? kMinLane : kStageLane1;
+                          : T::kConst0 ? (kGradF || kCrs ? 0 : kStageMinLaneC0)
+                          : kGradF ? kStageMinLaneFp
+                          : kCrs ? kStageMinLaneCrs : kStageMinLane;
+  constexpr int kStageLane = kPadLane > kStageLane1 ? kPadLane : kStageLane1;
   __shared__ double stage[kWPB][kWave * kStageLane];
 
   constexpr bool kC0J = T::kConst0 && kJac;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
   const int64_t num_chunks = (a.n + kWave - 1) / kWave;
-  const int64_t wg = (T::kXcdMap || (CSE_XCD_MAP != 0 && kJac)) ? XcdContiguous(blockIdx.x, gridDim.x)
-                                                                 : (int64_t)blockIdx.x;
-  const int64_t c = wg * kWPB + wave;
+  const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
   double* partial_dst = a.partials + c;
   if (c >= num_chunks) {
     if (lane == 0) *partial_dst = 0.0;  // the group's partial slots are 4 per workgroup
@@ -812,78 +681,26 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     fb[4] = a.fbase[c + 2 < num_chunks ? c + 2 : num_chunks];
   }
 
-  if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(2);
-  unsigned long long pt[5] = {0, 0, 0, 0, 0};  // T::kProbe stamps
-  auto stamp = [&](int k) {
-    if constexpr (T::kProbe) pt[k] = __builtin_amdgcn_s_memtime();
-  };
-  if constexpr (T::kProbe) {
-    stamp(0);
-    pt[4] = __builtin_amdgcn_s_memrealtime();
-  }
   AffineInputs<K> in;
   if constexpr (kCoop == 2) {
     int2 id;
     if constexpr (Tr::NB == 2) {
       const long long b = __builtin_nontemporal_load(reinterpret_cast<const long long*>(a.ids) + i);
       id = make_int2((int)b, (int)(b >> 32));
-      if constexpr (T::kProbe) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stamp(1);
-      }
-#ifdef CSE_TUNING
-      if constexpr (T::kScalarIds && kWPB == 1) {
-        if (nw == kWave) {  // uniform branch: the whole chunk exists
-          typedef int cse_s16 __attribute__((ext_vector_type(16)));
-          const uint64_t addr = reinterpret_cast<uint64_t>(a.ids + 2 * i0);
-          const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
-          const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
-          const uint64_t base = ((uint64_t)hi << 32) | lo;
-          int cx = 0;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {  // 4 x 16 dwords = 32 (camera, point) pairs per half
-            cse_s16 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(v[k]) : "s"(base), "i"(256 * h + 64 * k));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(cx) : "s"(v[k][2 * j]), "i"(32 * h + 8 * k + j));
-          }
-          id.x = cx;
-        }
-      }
-#endif
     } else {
       id = LoadIds<K>(a, i);
     }
-#ifdef CSE_TUNING
-    if constexpr (T::kDiag == 2 || T::kDiag == 3) {  // diagnostic: no camera gather
-      GatherDataAndSlot1<K, true>(a, i, id, &in);
-      const double* row = a.packed0;
-#pragma unroll
-      for (int k = 0; k < Tr::X0; ++k) in.x0[k] = row[k];
-      in.id0 = id.x;
-      in.id1 = id.y;
-    } else
-#endif
-    if constexpr (T::kEarlyObs || T::kRegGather ||
-                         (!kJac && Tr::D == 2 && Tr::NB == 2 && T::kCamStride == 0 && !T::kDmaOwn)) {
+    if constexpr (!kJac && Tr::D == 2 && Tr::NB == 2) {
       // Residual-only and cost-only evaluations issue the observation load
       // with the ids load (1.5-2 % faster, profiles/round2/s4h; the
       // Jacobian kernel is 4 % slower that way, s4c).
-      GatherEarly<K, T::kRegGather>(a, i, id, &in, st, lane);
+      GatherEarly<K>(a, i, id, &in, st, lane);
     } else {
-      GatherCoopDma<K, T::kCamStride, T::kDmaOwn>(a, i, id, &in, st, lane);
+      GatherCoopDma<K>(a, i, id, &in, st, lane);
     }
   } else {
     GatherCoop<K>(a, i, LoadIds<K>(a, i), &in, st, lane);
   }
-  if constexpr (T::kPrio == 2) __builtin_amdgcn_s_setprio(0);
-  stamp(2);
   // The chunk bounds' first use, after the gather: their scalar loads were
   // issued before it and have long arrived (without the pin the compiler
   // compares them right away and waits for them before the gather starts).
@@ -894,24 +711,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       asm volatile("" : "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]), "+v"(fb[4]));
   }
   double r[NR], J0[NR * S0], J1[NR * S1p];
-  bool ok;
-#ifdef CSE_TUNING
-  if constexpr (T::kDiag == 1 || T::kDiag == 3) {  // diagnostic: a few additions, no functor
-    double t = in.x1[0] + in.x1[S1 > 1 ? 1 : 0];
-#pragma unroll
-    for (int k = 0; k < S0; ++k) t += in.x0[k];
-#pragma unroll
-    for (int k = 0; k < NR; ++k) r[k] = in.d[k < Tr::D ? k : 0] + t;
-#pragma unroll
-    for (int k = 0; k < NR * S0; ++k) J0[k] = t * (k + 1);
-#pragma unroll
-    for (int k = 0; k < NR * S1p; ++k) J1[k] = t * (k + 2);
-    ok = true;
-  } else
-#endif
-  {
-    ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
-  }
+  bool ok = EvaluateFunctor<K, kJac>(in.d, in.x0, in.x1, r, J0, J1);
   if (ok && a.check_finite) {
     bool bad = AnyNonFinite<NR>(r);
     if constexpr (kJac) bad = bad || AnyNonFinite<NR * S0>(J0) || AnyNonFinite<NR * S1>(J1);
@@ -923,7 +723,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   bool act0 = true;  // slot-0 block active (T::kConst0: from its bit)
   if constexpr (T::kConst0) {
     static_assert(kCoop == 2, "constant slot-0 blocks: the repacked table");
-    if constexpr ((Tr::X0 & 1) != 0 && !T::kDmaOwn) {
+    if constexpr ((Tr::X0 & 1) != 0) {
       act0 = in.x0pad == 0.0;  // the flag came with the row (RepackSlot0Kernel)
     } else {
       const uint32_t k0 = (uint32_t)(in.id0 - a.packed0_lo);
@@ -1099,10 +899,8 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       }
       const cse_v4i qr = AsV4i(r[0], r[1]);
       double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;
-      cse_v4i sq[2], pq[2];
-      double *gp = nullptr, *sp = nullptr, *pc = nullptr;
-      bool pc_write = false;
-      constexpr bool kPointCopy = kGradF && T::kNoContrib && CSE_POINT_COPY != 0;
+      cse_v4i sq[2];
+      double *gp = nullptr, *sp = nullptr;
       // gradient_mode 3: the slot-0 contributions J0^T r of the chunk's own
       // blocks (10 doubles each, block order), staged like the cells.
       constexpr bool kContribC0 = kGradF && !T::kNoContrib;
@@ -1134,12 +932,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         sq[1] = AsV4i(fg.g1[2], fg.g1[3]);
         gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
         sp = a.gside + 4 * fg.entry;
-        if constexpr (kPointCopy) {
-          pq[0] = AsV4i(in.x1[0], in.x1[1]);
-          pq[1] = AsV4i(in.x1[2], 0.0);
-          pc_write = a.ppad != nullptr && fg.run_end;
-          pc = a.ppad + 4LL * (in.id1 - a.ppad_lo);
-        }
       }
       double* v_partial = partial_dst;
       double v_wsum = wsum;
@@ -1157,12 +949,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
             StoreNt16<0, 1>(sp, sq[0]);
             StoreNt16<16, 1>(sp, sq[1]);
           }
-          if constexpr (kPointCopy) {
-            if (pc_write) {
-              StoreNt16<0, 1>(pc, pq[0]);
-              StoreNt16<16, 1>(pc, pq[1]);
-            }
-          }
         }
       };
       // ---- every store of the wave ----
@@ -1171,12 +957,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       // neutral, profiles/round4/r4s5.)
       if (jacw && lane < 8) StoreNt16<0, 1>(ws, qs);
       if (jacw) {
-        if constexpr (!kCrs && CSE_C0_E_FIRST != 0) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
+        if constexpr (!kCrs) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
         if (whole)
           SegmentStoresMasked<0, kQF>(wf0, wf1, qf, 0, kQF * kWave);  // no lane masked
         else
           SegmentStoresMasked<0, kQF>(wf0, wf1, qf, lane, P);
-        if constexpr (!kCrs && CSE_C0_E_FIRST == 0) SegmentStoresMasked<0, kQE>(we0, we0, qe, lane, kPE);
       }
       if (a.residuals) StoreNt16<0>(rdst, qr);  // a full chunk: every lane active
       store_g();
@@ -1195,10 +980,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       if constexpr (kGradF) {
         KeepAlive<2>(sq);
         asm volatile("" ::"v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
-        if constexpr (kPointCopy) {
-          KeepAlive<2>(pq);
-          asm volatile("" ::"v"(pc));
-        }
       }
       return;
     }
@@ -1230,15 +1011,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
         e[0] = e[1] = e[2] = 0.0;
         e[3] = fg.g1[3];
       }
-      if constexpr (T::kNoContrib && CSE_POINT_COPY != 0) {
-        if (a.ppad && fg.run_end) {
-          double* pc = a.ppad + 4LL * (in.id1 - a.ppad_lo);
-          pc[0] = in.x1[0];
-          pc[1] = in.x1[1];
-          pc[2] = in.x1[2];
-          pc[3] = 0.0;
-        }
-      }
     }
     if (lane == 0) {
       *partial_dst = wsum;
@@ -1247,7 +1019,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     return;
   }
 
-  if constexpr (T::kPrio >= 1) __builtin_amdgcn_s_setprio(2);
   // Stage the Jacobian, read it back as 16-byte pieces in segment order.
   constexpr int kQ0 = kJac ? (kCrs ? NR * N / 2 : NR * S0 / 2) : 0;  // pieces per lane, seg 0 (F)
   constexpr int kQ1 = (kJac && !kCrs && S1 > 0) ? NR * S1 / 2 : 0;   // seg 1 (E cells)
@@ -1283,15 +1054,15 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
           // the second half, in the same LDS.  FastTail guarantees NR * N
           // even, so the halves split on a piece boundary.
           constexpr int kHalf = kWave / 2 * NR * N / 2;  // pieces per half
-          hp0 = SectorHeadPieces<kA>(seg0);
+          hp0 = SectorHeadPieces(seg0);
           if (lane < kWave / 2) stage_rows(st + lane * NR * N);
           __builtin_amdgcn_wave_barrier();
-          ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, 0, kHalf, q0);
+          ReadSegmentPiecesRange<kQ0>(st, hp0, lane, 0, kHalf, q0);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
           if (lane >= kWave / 2) stage_rows(st + (lane - kWave / 2) * NR * N);
           __builtin_amdgcn_wave_barrier();
-          ReadSegmentPiecesRange<kQ0, kA>(st, hp0, lane, kHalf, 2 * kHalf, q0);
+          ReadSegmentPiecesRange<kQ0>(st, hp0, lane, kHalf, 2 * kHalf, q0);
         } else {
           stage_rows(st + lane * NR * N);
         }
@@ -1300,7 +1071,7 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 #pragma unroll
         for (int p = 0; p < NR * S0; ++p) st[lane * NR * S0 + p] = J0[p];
         if constexpr (S1 > 0) {
-          if constexpr (kLdsE && !kTwo) {
+          if constexpr (!kTwo) {
 #pragma unroll
             for (int k = 0; k < NR; ++k)
 #pragma unroll
@@ -1312,11 +1083,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       }
       if constexpr (!kTwoCrs) {
         __builtin_amdgcn_wave_barrier();
-        hp0 = SectorHeadPieces<kA>(seg0);
-        ReadSegmentPieces<kQ0, kA>(st, hp0, lane, q0);
+        hp0 = SectorHeadPieces(seg0);
+        ReadSegmentPieces<kQ0>(st, hp0, lane, q0);
       }
       if constexpr (kQ1 > 0) {
-        hp1 = SectorHeadPieces<kA>(seg1);
+        hp1 = SectorHeadPieces(seg1);
         if constexpr (kTwo) {
           // Second round: the E cells in the LDS the F pieces came from.
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1326,13 +1097,9 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
 #pragma unroll
             for (int cc = 0; cc < S1; ++cc) st[lane * NR * S1 + k * S1 + cc] = J1[k * S1p + cc];
           __builtin_amdgcn_wave_barrier();
-          ReadSegmentPieces<kQ1, kA>(st, hp1, lane, q1);
-        } else if constexpr (kLdsE) {
-          ReadSegmentPieces<kQ1, kA>(st + kWave * NR * S0, hp1, lane, q1);
+          ReadSegmentPieces<kQ1>(st, hp1, lane, q1);
         } else {
-          // The lane's own cell, row-major (NR x S1, S1p == S1 here).
-#pragma unroll
-          for (int j = 0; j < kQ1; ++j) q1[j] = AsV4i(J1[2 * j], J1[2 * j + 1]);
+          ReadSegmentPieces<kQ1>(st + kWave * NR * S0, hp1, lane, q1);
         }
       }
     }
@@ -1349,18 +1116,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     sq[1] = AsV4i(fg.g1[2], fg.g1[3]);
     gp = a.gfused + a.delta_base[1] + 3LL * fg.key;
     sp = a.gside + 4 * fg.entry;
-  }
-  constexpr bool kPointCopy = kGradF && T::kNoContrib && CSE_POINT_COPY != 0;
-  cse_v4i pq[2];
-  double* pc = nullptr;
-  bool pc_write = false;
-  if constexpr (kPointCopy) {
-    if constexpr (Tr::S1 == 3) {
-      pq[0] = AsV4i(in.x1[0], in.x1[1]);
-      pq[1] = AsV4i(in.x1[2], 0.0);
-    }
-    pc_write = a.ppad != nullptr && fg.run_end;
-    pc = a.ppad + 4LL * (in.id1 - a.ppad_lo);
   }
   if constexpr (kContrib) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1391,17 +1146,11 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   if (jac) {
     f0 = seg0 + 2 * (lane + hp0) + 512;
     f1 = seg0 + 2 * (lane + hp0) + 1536;
-    flast = seg0 + 2 * LastPiece<(kQ0 > 0 ? kQ0 : 1), kA>(lane, hp0);
+    flast = seg0 + 2 * LastPiece<(kQ0 > 0 ? kQ0 : 1)>(lane, hp0);
     if constexpr (kQ1 > 0) {
-      if constexpr (kLdsE) {
-        e0 = seg1 + 2 * (lane + hp1) + 512;
-        e1 = seg1 + 2 * (lane + hp1) + 1536;
-        elast = seg1 + 2 * LastPiece<kQ1, kA>(lane, hp1);
-      } else {
-        e0 = seg1 + NR * S1 * lane;  // the lane's own 48-byte cell
-        e1 = e0;
-        elast = e0;
-      }
+      e0 = seg1 + 2 * (lane + hp1) + 512;
+      e1 = seg1 + 2 * (lane + hp1) + 1536;
+      elast = seg1 + 2 * LastPiece<kQ1>(lane, hp1);
     }
   }
   // The partial's address and value in VGPRs now, not after the tail.
@@ -1410,42 +1159,25 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
   asm volatile("" : "+v"(v_partial), "+v"(v_wsum));
   asm volatile("" ::"v"(f0), "v"(f1), "v"(e0), "v"(e1), "v"(rdst), "v"(flast), "v"(elast));
 
-  stamp(3);
   // ---- every store of the wave, back to back ----
   auto store_f = [&]() {
-#ifdef CSE_TUNING
-    if constexpr (T::kDiag == 4) return;  // diagnostic: no Jacobian stores
-#endif
     if (jac) {
-      SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0), T::kFPol>(f0, f1, q0);
-      if constexpr (kQ0 > 0) StoreNt16<0, T::kFPol>(flast, q0[kQ0 - 1]);
+      SegmentStoresFrom<0, (kQ0 > 0 ? kQ0 - 1 : 0)>(f0, f1, q0);
+      if constexpr (kQ0 > 0) StoreNt16<0>(flast, q0[kQ0 - 1]);
     }
   };
   auto store_e = [&]() {
-#ifdef CSE_TUNING
-    if constexpr (T::kDiag == 4 || T::kDiag == 5) return;  // diagnostic: no E stores
-#endif
     if constexpr (kQ1 > 0) {
       if (!jac) return;
-      if constexpr (kLdsE) {
-        SegmentStoresFrom<0, kQ1 - 1, T::kEPol>(e0, e1, q1);
-        StoreNt16<0, T::kEPol>(elast, q1[kQ1 - 1]);
-      } else {
-        // Per-lane pieces at a 48-byte lane stride: each instruction covers
-        // a third of every line of the segment, default policy so that the
-        // three partial writes of a line merge in L2.
-        if constexpr (kQ1 >= 1) StoreNt16<0, 1>(e0, q1[0]);
-        if constexpr (kQ1 >= 2) StoreNt16<16, 1>(e0, q1[1]);
-        if constexpr (kQ1 >= 3) StoreNt16<32, 1>(e0, q1[2]);
-        static_assert(kQ1 <= 3, "E cells of at most 48 bytes");
-      }
+      SegmentStoresFrom<0, kQ1 - 1>(e0, e1, q1);
+      StoreNt16<0>(elast, q1[kQ1 - 1]);
     }
   };
   auto store_r = [&]() {
     if (a.residuals) {  // a kernel argument: a scalar branch, no VALU after the stores
-      if constexpr (kQr >= 1) StoreNt16<0, T::kRPol>(rdst, qr[0]);
-      if constexpr (kQr >= 2) StoreNt16<16, T::kRPol>(rdst, qr[1]);
-      if constexpr (kQr >= 3) StoreNt16<32, T::kRPol>(rdst, qr[2]);
+      if constexpr (kQr >= 1) StoreNt16<0>(rdst, qr[0]);
+      if constexpr (kQr >= 2) StoreNt16<16>(rdst, qr[1]);
+      if constexpr (kQr >= 3) StoreNt16<32>(rdst, qr[2]);
     }
   };
   auto store_g = [&]() {  // the fused gradient's rows and entries (exec-masked)
@@ -1458,12 +1190,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
       if (fg.writer) {
         StoreNt16<0, 1>(sp, sq[0]);
         StoreNt16<16, 1>(sp, sq[1]);
-      }
-      if constexpr (kPointCopy) {
-        if (pc_write) {
-          StoreNt16<0, 1>(pc, pq[0]);
-          StoreNt16<16, 1>(pc, pq[1]);
-        }
       }
     }
   };
@@ -1489,18 +1215,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     StoreB64(v_partial, v_wsum);
     if (failed) StoreB32(status_dst, 1);
   }
-  if constexpr (T::kProbe) {
-    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
-    if (lane == 0 && a.probe) {
-      unsigned long long* o = a.probe + 8 * c;
-      o[0] = pt[1] - pt[0];  // the ids load
-      o[1] = pt[2] - pt[1];  // the camera gather, observations and points
-      o[2] = pt[3] - pt[2];  // functor, loss, staging, addresses
-      o[3] = t4 - pt[3];     // issuing the store tail
-      o[4] = pt[4];          // s_memrealtime at the start (100 MHz)
-      o[5] = 1;
-    }
-  }
   KeepAlive<(kQ0 > 0 ? kQ0 : 1)>(q0);
   KeepAlive<(kQ1 > 0 ? kQ1 : 1)>(q1);
   KeepAlive<kQr>(qr);
@@ -1510,10 +1224,6 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     if constexpr (kContrib) KeepAlive<kGQ>(gq);
     KeepAlive<2>(sq);
     asm volatile("" ::"v"(cb0), "v"(gp), "v"(sp), "v"(fg.g1[0]), "v"(fg.g1[1]), "v"(fg.g1[2]));
-    if constexpr (kPointCopy) {
-      KeepAlive<2>(pq);
-      asm volatile("" ::"v"(pc));
-    }
   }
 }
 
@@ -1521,34 +1231,16 @@ template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T = Shipped
 __global__ __launch_bounds__(kBlockThreads) void EvaluateAffineChunks(const GroupArgs a) {
   AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T>(a);
 }
-// kWPB waves per workgroup (A/B builds, CSE_CHUNKS_WPB).
-template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T, int kWPB>
-__global__ __launch_bounds__(kWPB * kWave) void EvaluateAffineChunksW(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T, kWPB>(a);
-}
-
-// The shipped BSM Jacobian kernel of two-slot kinds: two-round staging (36
-// KiB of LDS a workgroup, 4 per CU) held to 4 waves per SIMD (128 VGPRs).
-template <class K, int kLoss, int kCoop, class T = ShippedTune>
-__global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRound(const GroupArgs a) {
-  static_assert(kTwoRoundBsm<K>, "two-slot kinds");
-  AffineChunkBody<K, kLoss, true, false, kCoop, false, T>(a);
-}
-
-// The same with one wave per workgroup (9 KiB of LDS each, 16 per CU): each
-// wave is dispatched and retired on its own, so the CU's waves do not start
-// and reach their store tails in groups of four.
-#ifndef CSE_W1_WAVES_PER_EU
-#define CSE_W1_WAVES_PER_EU 4
-#endif
-// The Snavely camera's Jacobian by hand fits 5 waves per SIMD (88-90 VGPRs,
-// no spills); the held-camera (kConst0) forms and the Jet-based kinds stay at
-// 4 (at 5 the quaternion kinds spill 130-160 bytes a lane).
-#ifndef CSE_FP_W1_WAVES
-#define CSE_FP_W1_WAVES 4
-#endif
-template <class K, class T, int kWaves = CSE_W1_WAVES_PER_EU>
-constexpr int kW1Waves = (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0 && !T::kConst0) ? kWaves : 4;
+// The shipped BSM Jacobian kernel of two-slot kinds: two-round staging (9
+// KiB of LDS a wave) with one wave per workgroup (16 per CU): each wave is
+// dispatched and retired on its own, so the CU's waves do not start and
+// reach their store tails in groups of four (1.447-1.454 -> 1.422-1.427 ms
+// against four-wave workgroups, profiles/round3/w1).  Held to 4 waves per
+// SIMD (128 VGPRs); the held-camera (kConst0) forms and the Jet-based kinds
+// likewise (at 5 the quaternion kinds spill 130-160 bytes a lane).
+constexpr int kW1WavesPerEu = 4;
+template <class K, class T>
+constexpr int kW1Waves = kW1WavesPerEu;
 template <class K, int kLoss, int kCoop, class T = ShippedTune>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T>))) void
 EvaluateAffineChunksTwoRoundW1(const GroupArgs a) {
@@ -1556,26 +1248,14 @@ EvaluateAffineChunksTwoRoundW1(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, false, kCoop, false, T, 1>(a);
 }
 
-// The shipped CRS Jacobian kernel: rows staged in two half-waves (24 KiB of
-// LDS a workgroup) and held to 4 waves per SIMD (128 VGPRs), as the BSM
-// kernel; one-round staging took 48 KiB and 130 VGPRs (3 waves per SIMD).
-template <class K, int kLoss, int kCoop>
-__global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksTwoRoundCrs(const GroupArgs a) {
-  AffineChunkBody<K, kLoss, true, true, kCoop, false, ShippedTune>(a);
-}
-// The same with one wave per workgroup (6 KiB of LDS each).
+// The shipped CRS Jacobian kernel: rows staged in two half-waves (6 KiB of
+// LDS a wave, one wave per workgroup) and held to 4 waves per SIMD (128
+// VGPRs), as the BSM kernel; one-round staging took 130 VGPRs (3 waves per
+// SIMD).
 template <class K, int kLoss, int kCoop, class T = ShippedTune>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T>))) void
 EvaluateAffineChunksTwoRoundCrsW1(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, true, kCoop, false, T, 1>(a);
-}
-
-// The same held to at least kMinWaves waves per SIMD (a register bound:
-// 4 waves = 128 VGPRs), for settings whose LDS admits more workgroups.
-template <class K, int kLoss, bool kJac, bool kCrs, int kCoop, class T, int kMinWaves>
-__global__ __launch_bounds__(kBlockThreads, kMinWaves) void EvaluateAffineChunksBounded(
-    const GroupArgs a) {
-  AffineChunkBody<K, kLoss, kJac, kCrs, kCoop, false, T>(a);
 }
 
 // The fused-gradient form of the hot kernel, held to 3 waves per SIMD
@@ -1589,26 +1269,15 @@ EvaluateAffineChunksFused(const GroupArgs a) {
 
 // The fused gradient's points-only form: the slot-1 rows and boundary
 // entries as above, no slot-0 contributions (CameraGradientKernel computes
-// the slot-0 sums).  Without the contribution registers both forms fit 128
-// VGPRs and run at 4 waves per SIMD (CRS with the half-wave staging: 2.33 ->
-// 2.25 ms against 3 waves, profiles/round2/s5l).
+// the slot-0 sums).  Without the contribution registers it fits 128 VGPRs
+// and runs at 4 waves per SIMD (CRS with the half-wave staging: 2.33 ->
+// 2.25 ms against 3 waves, profiles/round2/s5l), one wave per workgroup
+// (gradient evaluation 2.147-2.153 -> 2.107-2.109 ms, profiles/round3/w1).
 template <class K, int kLoss, bool kCrs, class T = PointsOnlyTune>
-__global__ __launch_bounds__(kBlockThreads, 4) void EvaluateAffineChunksFusedPoints(
-    const GroupArgs a) {
-  AffineChunkBody<K, kLoss, true, kCrs, 2, true, T>(a);
-}
-// One wave per workgroup (A/B builds, CSE_FUSEDPOINTS_W1).
-template <class K, int kLoss, bool kCrs, class T = PointsOnlyTune>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T, CSE_FP_W1_WAVES>))) void
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kW1Waves<K, T>))) void
 EvaluateAffineChunksFusedPointsW1(const GroupArgs a) {
   AffineChunkBody<K, kLoss, true, kCrs, 2, true, T, 1>(a);
 }
-
-// The camera-order re-evaluation's Jacobian: by hand (1) or through Jet<9>
-// with the point constant (0).
-#ifndef CSE_BY_HAND_CAMGRAD
-#define CSE_BY_HAND_CAMGRAD 1
-#endif
 
 // Slot-0 (camera) part of the fused gradient, by re-evaluation in camera
 // order.  The evaluation kernel runs in block (point) order, in which a
@@ -1647,21 +1316,18 @@ struct CamGradArgs {
   const double* packed0;
   int32_t packed_lo;
   int32_t packed_stride;
-  // The points kernel's 32-byte-stride copy of slot 1 (GroupArgs::ppad), or
-  // null: gather from the state.
-  const double* ppad;
-  int32_t ppad_lo;
 };
 
 // r and the slot-0 Jacobian (NR x S0, row-major) of one block, the slot-1
 // parameters held constant (AutoDifferentiate with only slot 0 seeded; a
 // slot-0 manifold maps the X0 ambient partials to the S0 tangent columns).
+// The Snavely camera's by hand (SnavelyJacobianByHand), as the evaluation.
 template <class K>
 __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
                                               const double* x1, double* r, double* J0) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1;
-  if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0 && CSE_BY_HAND_CAMGRAD != 0) {
+  if constexpr (std::is_same<K, SnavelyKind>::value) {
     double J1[NR * S1];  // dead: the point's partials are not needed here
     SnavelyJacobianByHand(d, x0, x1, r, J0, J1);
     return;
@@ -1684,26 +1350,13 @@ __device__ __forceinline__ void EvaluateSlot0(const double* d, const double* x0,
   }
 }
 
-// CameraGradientKernel's camera rows for the Snavely camera: by the reverse
-// sweep SnavelyCameraRowVjp (1) or by forming J0 by hand and contracting it
-// with the corrected residuals (0).
-#ifndef CSE_CAMGRAD_VJP
-#define CSE_CAMGRAD_VJP 0
-#endif
-template <class K>
-constexpr bool kCamGradVjp = std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0 && CSE_CAMGRAD_VJP != 0;
-// The sorted slot-1 ids streamed non-temporally (1) or with the default
-// policy (0), like the functor data.
-#ifndef CSE_CAMGRAD_NT_IDS
-#define CSE_CAMGRAD_NT_IDS 1
-#endif
-// CSE_CAMGRAD_WAVES: a lower bound on its waves per SIMD (A/B builds; 1 = the
-// compiler's choice, 158 VGPRs = 3 with the by-hand functor).
-#ifndef CSE_CAMGRAD_WAVES
-#define CSE_CAMGRAD_WAVES 1
-#endif
+// The camera rows are J0 formed (by hand for the Snavely camera) and
+// contracted with the corrected residuals (a reverse sweep measured no
+// faster); the sorted slot-1 ids and the functor data stream non-temporally.
+// Waves per SIMD: the compiler's choice (158 VGPRs = 3 with the by-hand
+// functor).
 template <class K, int kLoss, int kWPB = kWavesPerBlock>
-__global__ __launch_bounds__(kWPB * kWave) __attribute__((amdgpu_waves_per_eu(CSE_CAMGRAD_WAVES))) void
+__global__ __launch_bounds__(kWPB * kWave) __attribute__((amdgpu_waves_per_eu(1))) void
 CameraGradientKernel(const CamGradArgs g) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, S0 = Tr::S0, S1 = Tr::S1, S1p = Tr::S1p, D = Tr::D;
@@ -1743,42 +1396,13 @@ CameraGradientKernel(const CamGradArgs g) {
     for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int k = 0; k < D; ++k) d[u][k] = __builtin_nontemporal_load(g.sdata + qb[u] * D + k);
-      const int32_t id1 = CSE_CAMGRAD_NT_IDS ? __builtin_nontemporal_load(g.sid1 + qb[u]) : g.sid1[qb[u]];
-      if constexpr (S1 == 3) {
-        if (g.ppad) {  // the 32-byte-stride copy: one sector per point
-          const double* p1 = g.ppad + 4LL * (id1 - g.ppad_lo);
-          const double2 xy = *reinterpret_cast<const double2*>(p1);
-          x1[u][0] = xy.x;
-          x1[u][1] = xy.y;
-          x1[u][2] = p1[2];
-          continue;
-        }
-      }
+      const int32_t id1 = __builtin_nontemporal_load(g.sid1 + qb[u]);
       const double* p1 = g.state + g.state_base1 + (int64_t)S1 * id1;
 #pragma unroll
       for (int k = 0; k < S1; ++k) x1[u][k] = p1[k];
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      if constexpr (kCamGradVjp<K>) {
-        // the camera row by a reverse sweep (SnavelyCameraRowVjp)
-        double r[NR], gv[S0];
-        const bool robust = (kLoss != kLossTrivial || g.loss.scaled) && g.apply_loss;
-        SnavelyCameraRowVjp(
-            d[u], x0, x1[u],
-            [&](double sq) {
-              if (!robust) return 1.0;
-              double rho[3];
-              EvaluateLoss<kLoss>(g.loss, sq, rho);
-              return rho[1];
-            },
-            r, gv);
-        if (live[u]) {
-#pragma unroll
-          for (int c = 0; c < S0; ++c) acc[c] += gv[c];
-        }
-        continue;
-      }
       double r[NR], J0[NR * S0], J1[NR * S1p];
       EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
 #pragma unroll

@@ -285,78 +285,6 @@ CSE_HD bool SnavelyJacobianByHand(const double* obs, const double* cam, const do
   return true;
 }
 
-// The camera row of one block's gradient, g0 = J0^T v, by the reverse sweep
-// of the same arithmetic (a vector-Jacobian product) instead of forming J0:
-// v = rho'(|r|^2) r when a robust loss applies (the Corrector's J~^T r~
-// equals rho' J^T r, corrector.h:82-213), else r.  With the names of
-// SnavelyJacobianByHand: g_f = D (x.v), g_l1 = f r2 (x.v), g_l2 = f r2^2 (x.v),
-// g_t = h = B^T A v, g_aa = G^T h = aa (w.h) + c (aa.X) h + z x h.  About a
-// third of the FP64 operations of forming J0 and contracting it.
-// rho1(sq) returns rho' (1 without a robust loss); r receives the residuals.
-template <class Rho1>
-CSE_HD void SnavelyCameraRowVjp(const double* obs, const double* cam, const double* X, Rho1 rho1,
-                                double* r, double* g) {
-  const double a0 = cam[0], a1 = cam[1], a2 = cam[2];
-  const double u = a0 * a0 + a1 * a1 + a2 * a2;
-  double s, c, ds, dc, p[3];
-  const double q0 = a1 * X[2] - a2 * X[1], q1 = a2 * X[0] - a0 * X[2], q2 = a0 * X[1] - a1 * X[0];
-  const double m0 = a1 * q2 - a2 * q1, m1 = a2 * q0 - a0 * q2, m2 = a0 * q1 - a1 * q0;
-  if (u <= 1.0) {
-    RodriguesFactors(u, &s, &c, &ds, &dc);
-    p[0] = X[0] + s * q0 + c * m0;
-    p[1] = X[1] + s * q1 + c * m1;
-    p[2] = X[2] + s * q2 + c * m2;
-  } else {
-    const double theta = jhypot(a0, a1, a2);
-    double st, ct;
-    jsincos(theta, &st, &ct);
-    const double ti = 1.0 / theta;
-    const double w0 = a0 * ti, w1 = a1 * ti, w2 = a2 * ti;
-    const double x0 = w1 * X[2] - w2 * X[1], x1 = w2 * X[0] - w0 * X[2], x2 = w0 * X[1] - w1 * X[0];
-    const double tmp = (w0 * X[0] + w1 * X[1] + w2 * X[2]) * (1.0 - ct);
-    p[0] = X[0] * ct + x0 * st + w0 * tmp;
-    p[1] = X[1] * ct + x1 * st + w1 * tmp;
-    p[2] = X[2] * ct + x2 * st + w2 * tmp;
-    s = st * ti;
-    c = (1.0 - ct) / u;
-    ds = (ct - s) / (2.0 * u);
-    dc = (s - 2.0 * c) / (2.0 * u);
-  }
-  p[0] += cam[3];
-  p[1] += cam[4];
-  p[2] += cam[5];
-  const double ni = -1.0 / p[2];
-  const double xp = p[0] * ni, yp = p[1] * ni;
-  const double f = cam[6], l1 = cam[7], l2 = cam[8];
-  const double r2 = xp * xp + yp * yp;
-  const double D = 1.0 + r2 * (l1 + l2 * r2);
-  r[0] = f * D * xp - obs[0];
-  r[1] = f * D * yp - obs[1];
-  const double k = rho1(r[0] * r[0] + r[1] * r[1]);
-  const double v0 = k * r[0], v1 = k * r[1];
-  const double xv = xp * v0 + yp * v1;
-  g[6] = D * xv;
-  g[7] = f * r2 * xv;
-  g[8] = f * r2 * r2 * xv;
-  // h = B^T A v, A v = f D v + fg x (x.v)
-  const double fD = f * D, fg = f * (2.0 * l1 + 4.0 * l2 * r2);
-  const double w0 = fD * v0 + fg * xp * xv, w1 = fD * v1 + fg * yp * xv;
-  const double h0 = ni * w0, h1 = ni * w1, h2 = ni * (xp * w0 + yp * w1);
-  g[3] = h0;
-  g[4] = h1;
-  g[5] = h2;
-  // G^T h
-  const double cd = c * (a0 * X[0] + a1 * X[1] + a2 * X[2]);
-  const double ww0 = 2.0 * (ds * q0 + dc * m0) - c * X[0];
-  const double ww1 = 2.0 * (ds * q1 + dc * m1) - c * X[1];
-  const double ww2 = 2.0 * (ds * q2 + dc * m2) - c * X[2];
-  const double z0 = s * X[0] + c * q0, z1 = s * X[1] + c * q1, z2 = s * X[2] + c * q2;
-  const double wh = ww0 * h0 + ww1 * h1 + ww2 * h2;
-  g[0] = a0 * wh + cd * h0 + (z1 * h2 - z2 * h1);
-  g[1] = a1 * wh + cd * h1 + (z2 * h0 - z0 * h2);
-  g[2] = a2 * wh + cd * h2 + (z0 * h1 - z1 * h0);
-}
-
 // SnavelyReprojectionErrorNoRadialDistortion<2, 7, 3>
 // (internal/ceres/evaluator_cuda_test.cu.cc:112-150).
 struct SnavelyNoDistortionKind {

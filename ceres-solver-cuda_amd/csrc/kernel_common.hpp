@@ -85,17 +85,9 @@ struct GroupArgs {
   double* gfused;
   double* gside;
   double* gcontrib;
-  // The fused gradient's points-only form also leaves a copy of the slot-1
-  // blocks at a 32-byte stride, (x, y, z, 0) at ppad + 4 * (id - ppad_lo),
-  // for CameraGradientKernel's gather (one 64-byte sector per point); null =
-  // none.
-  double* ppad;
-  int32_t ppad_lo;
   LossParams loss;
   int apply_loss;
   int check_finite;
-  int num_cus;  // compute units of the device (persistent launches)
-  unsigned long long* probe;  // tuning build: per-wave cycle accounting (pipeline kernel)
   // kLossUser: the bytes of the group's loss object (cse_loss.user).
   double user_loss[kUserLossDoubles];
 };
@@ -103,7 +95,7 @@ struct GroupArgs {
 // Layout tag of GroupArgs, checked when a user functor kind registers
 // kernels compiled in another TU (cse_register_functor): bump on any change
 // to the struct.
-constexpr uint64_t kGroupArgsTag = 0x6373654761310001ull;
+constexpr uint64_t kGroupArgsTag = 0x6373654761310002ull;
 
 // Compile-time shape of a functor kind: kR residuals, NB parameter blocks
 // of sizes kSizes[0..NB) concatenated into N columns.
@@ -273,17 +265,13 @@ __device__ __forceinline__ void WaveStore(const double* lds, double* dst, int co
   }
 }
 
-// The Snavely camera's Jacobian on the device: by hand
-// (SnavelyJacobianByHand, CSE_BY_HAND 1) or through the seeded Jets (0).
-#ifndef CSE_BY_HAND
-#define CSE_BY_HAND 1
-#endif
-
 // AutoDifferentiate (include/ceres/internal/autodiff.h:314-381) for the
 // two-slot affine kernels: seed one Jet per parameter with its unit vector,
 // pre-fill the outputs with kImpossibleValue (:355-360), run the functor,
 // split the partials into the row-major per-block Jacobians.  kJac = false
-// runs the functor on plain doubles.
+// runs the functor on plain doubles.  The Snavely camera's Jacobian is the
+// same product rule written out once (SnavelyJacobianByHand); its Jet form
+// is the distinct kind SnavelyJetKind (cse_options.jacobian_form).
 template <class K, bool kJac>
 CSE_HD bool EvaluateFunctor(const double* d, const double* x0, const double* x1, double* r,
                             double* J0, double* J1) {
@@ -291,7 +279,7 @@ CSE_HD bool EvaluateFunctor(const double* d, const double* x0, const double* x1,
   constexpr int NR = Tr::NR, S0 = Tr::S0, X0 = Tr::X0, S1 = Tr::S1, S1p = Tr::S1p, N = X0 + S1;
   if constexpr (kJac) {
 #ifdef __HIP_DEVICE_COMPILE__
-    if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0)
+    if constexpr (std::is_same<K, SnavelyKind>::value)
       return SnavelyJacobianByHand(d, x0, x1, r, J0, J1);
 #endif
     Jet<N> j0[X0], j1[S1p], out[NR];
@@ -333,7 +321,7 @@ CSE_HD bool EvaluateFunctorFlat(const double* d, const double* x, double* r, dou
 #ifdef __HIP_DEVICE_COMPILE__
     // The same arithmetic as the affine kernels (EvaluateFunctor): the two
     // store paths write bit-identical Jacobians.
-    if constexpr (std::is_same<K, SnavelyKind>::value && CSE_BY_HAND != 0) {
+    if constexpr (std::is_same<K, SnavelyKind>::value) {
       double J0[18], J1[6];
       const bool ok = SnavelyJacobianByHand(d, x, x + 9, r, J0, J1);
 #pragma unroll
@@ -418,22 +406,13 @@ __device__ __forceinline__ cse_v4i AsV4i(double a, double b) {
 // 16-byte store at base + kOff bytes (kOff in [-4096, 4095]).  kPol: the
 // cache policy, 0 = nt sc1 (streaming, not kept in the XCD's L2; 6-8 %
 // faster than nt alone on the evaluator's output stream, profiles/r02),
-// 1 = default policy, 2 = nt, 3 = sc0 sc1 nt, 4 = sc0 sc1 (tuning only).
+// 1 = default policy (small scattered stores whose lines neighbours share).
 template <int kOff, int kPol = 0>
 __device__ __forceinline__ void StoreNt16(double* base, const cse_v4i& d) {
   static_assert(kOff >= -4096 && kOff <= 4095, "global offset out of range");
+  static_assert(kPol == 0 || kPol == 1, "cache policies: 0 streaming, 1 default");
   if constexpr (kPol == 1)
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2" ::"v"(base), "v"(d), "i"(kOff)
-                 : "memory");
-  else if constexpr (kPol == 2)
-    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 nt" ::"v"(base), "v"(d), "i"(kOff)
-                 : "memory");
-  else if constexpr (kPol == 3)
-    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1 nt" ::"v"(base), "v"(d),
-                 "i"(kOff)
-                 : "memory");
-  else if constexpr (kPol == 4)
-    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1" ::"v"(base), "v"(d), "i"(kOff)
                  : "memory");
   else
     asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1 nt" ::"v"(base), "v"(d),
@@ -443,11 +422,11 @@ __device__ __forceinline__ void StoreNt16(double* base, const cse_v4i& d) {
 
 // Pieces kJ.. of a wave segment: piece j of lane l at b + 16 * (64 (j % 8))
 // - 4096 bytes, b = b0 for j < 8 and b1 after (1 KiB per instruction).
-template <int kJ, int kCount, int kPol = 0>
+template <int kJ, int kCount>
 __device__ __forceinline__ void SegmentStoresFrom(double* b0, double* b1, const cse_v4i* q) {
   if constexpr (kJ < kCount) {
-    StoreNt16<(kJ % 8) * 1024 - 4096, kPol>(kJ < 8 ? b0 : b1, q[kJ]);
-    SegmentStoresFrom<kJ + 1, kCount, kPol>(b0, b1, q);
+    StoreNt16<(kJ % 8) * 1024 - 4096>(kJ < 8 ? b0 : b1, q[kJ]);
+    SegmentStoresFrom<kJ + 1, kCount>(b0, b1, q);
   }
 }
 

@@ -15,8 +15,7 @@ using namespace cse;
 int main() {
   std::mt19937_64 rng(0xC0FFEE);
   std::uniform_real_distribution<double> U(-1.0, 1.0);
-  double worst_j = 0.0, worst_r = 0.0, worst_kind[5] = {0, 0, 0, 0, 0}, worst_vjp = 0.0;
-  bool residual_mismatch = false;
+  double worst_j = 0.0, worst_r = 0.0, worst_kind[5] = {0, 0, 0, 0, 0};
   int n = 0;
   for (int t = 0; t < 200000; ++t) {
     double cam[9], X[3], obs[2];
@@ -49,32 +48,11 @@ int main() {
       const double dr = std::fabs(r[k] - out[k].a) / std::fmax(1.0, std::fabs(out[k].a));
       if (dr > worst_r) worst_r = dr;
     }
-    // The camera row by the reverse sweep (SnavelyCameraRowVjp) against
-    // J0^T (rho' r) from the same by-hand J0, with a Huber-like weight.
-    {
-      double rv[2], g[9];
-      const double rho1 = 0.75;
-      SnavelyCameraRowVjp(obs, cam, X, [&](double) { return rho1; }, rv, g);
-      double gmax = 0.0, gref[9];
-      for (int c = 0; c < 9; ++c) {
-        gref[c] = rho1 * (J0[c] * r[0] + J0[9 + c] * r[1]);
-        gmax = std::fmax(gmax, std::fabs(gref[c]));
-      }
-      for (int c = 0; c < 9; ++c) {
-        const double d = std::fabs(g[c] - gref[c]) / (gmax > 0 ? gmax : 1.0);
-        if (d > worst_vjp) worst_vjp = d;
-      }
-      for (int k = 0; k < 2; ++k)
-        if (rv[k] != r[k]) residual_mismatch = true;
-    }
     ++n;
   }
   std::printf("per angle class (theta 0, ~1e-6, ~0.3, ~1.5, ~3): %.2e %.2e %.2e %.2e %.2e\n",
               worst_kind[0], worst_kind[1], worst_kind[2], worst_kind[3], worst_kind[4]);
   std::printf("byhand_check: %d blocks, worst Jacobian difference %.3e of the row's largest entry, "
               "worst residual difference %.3e\n", n, worst_j, worst_r);
-  std::printf("camera row by the reverse sweep: worst difference %.3e of the row's largest entry "
-              "(J0^T rho' r from the by-hand J0); residuals bit-equal: %s\n", worst_vjp,
-              residual_mismatch ? "no" : "yes");
-  return worst_j <= 1e-12 && worst_r <= 1e-12 && worst_vjp <= 1e-12 && !residual_mismatch ? 0 : 1;
+  return worst_j <= 1e-12 && worst_r <= 1e-12 ? 0 : 1;
 }

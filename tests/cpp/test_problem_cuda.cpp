@@ -115,7 +115,7 @@ static void RunFormat(JacobianFormat format) {
   oracle_program p{5, pb_size.data(), pb_tan.data(), pb_const.data(), pb_pj.data(), pj.data(),
                    5, kind.data(), lk.data(), la.data(), ls.data(), lsd.data(), pbeg.data(),
                    params.data(), dbeg.data(), data.data(),
-                   crs ? ORACLE_COMPRESSED_ROW : ORACLE_BLOCK_SPARSE, 0, 1};
+                   crs ? ORACLE_COMPRESSED_ROW : ORACLE_BLOCK_SPARSE, 0, 1, nullptr};
   oracle_sizes sz;
   EXPECT(oracle_sizes_of(&p, &sz) == 0);
   EXPECT(sz.num_jacobian_values == evaluator.NumJacobianValues());

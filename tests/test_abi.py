@@ -73,9 +73,9 @@ def test_no_cpu_fallback_in_the_product():
 
 
 def test_product_library_reads_no_environment():
-    """libcse.so has no getenv-selected kernels (tuning variants live only
-    in lib/libcse_tuning.so, built by `make tuning`): no CSE_* variable name
-    is in its read-only data, and it imports no getenv at all."""
+    """libcse.so has no getenv-selected kernels (round 6 removed the tuning
+    build altogether): no CSE_* variable name is in its read-only data, and it
+    imports no getenv at all."""
     from ceres_amd import _cse
     data = open(_cse.LIB_PATH, "rb").read()
     assert not re.findall(rb"CSE_[A-Z][A-Z_]+", data), re.findall(rb"CSE_[A-Z][A-Z_]+", data)[:5]

@@ -10,7 +10,7 @@ from ceres_amd import bal
 
 pytestmark = pytest.mark.gpu
 
-# Names of the variables older builds (and the tuning build) honour.
+# Names of the variables older builds (and the round-5 tuning build) honoured.
 STRAY = {"CSE_AFFINE_VARIANT": "21", "CSE_VALUES_VARIANT": "3", "CSE_WG_PER_CU": "1",
          "CSE_NO_DMA_GATHER": "1", "CSE_ATOMIC_GRADIENT": "1", "CSE_TUNE_VARIANT": "5",
          "CSE_PIPE_WAVES": "2", "CSE_STREAM_WAVES": "1", "CSE_TIMELINE": "/dev/null"}

@@ -68,7 +68,7 @@ def oracle(prog, kind_map=None, loss_map=None, threads=8, **kw):
 
 
 def small(C=16, P=600, O_=2300, seed=7):
-    return bal.synthetic((C, P, O_), seed=seed)
+    return bal.synthetic(C, P, O_, seed=seed)
 
 
 @pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])

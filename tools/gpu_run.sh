@@ -10,7 +10,6 @@
 #     "rocprof --no-cpu-baseline --steps 30 --warmup 3" \
 #     "rocprof-tests tests/test_parity_gpu.py -m slow" \
 #     "ab 3 jacobian plain:: jet::--jacobian-form=jet" \
-#     "variants 3 jacobian 0,80,81" \
 #     "configs" "pmc" "membench"
 #
 # Kinds:
@@ -24,8 +23,6 @@
 #                         directory under ceres-solver-cuda_amd/lib (empty =
 #                         lib/libcse.so), FLAGS extra ab_bench flags with '='
 #                         between flag and value and ',' between flags
-#   variants ROUNDS MODE V,V,.. [FLAGS]
-#                         tools/ab_bench.py over the tuning build's variants
 #   configs [LIST]        tools/run_configs.sh (LIST: newline-separated args)
 #   pmc [BENCH_ARGS]      per-kernel PMC passes (tools/gpu_pmc_kernels.sh); with
 #                         no BENCH_ARGS (the headline) also its HBM traffic JSON
@@ -84,12 +81,6 @@ for step in "$@"; do
           echo "$name r$r: $(summ $f)"
         done
       done ;;
-    variants)
-      read -r rounds mode vs flags <<< "$args"
-      f=$OUT/variants_$n.txt
-      timeout -k 10 900 python -u tools/ab_bench.py --variants $vs --rounds $rounds --steps 20 \
-        --mode $mode ${flags//=/ } > $f 2>&1 || { echo "variants rc=$?"; tail -8 $f; exit 1; }
-      grep "^#" $f; summ $f ;;
     configs)
       if [ -n "$args" ]; then CONFIGS="$args" TAG=$TAG/configs_$n bash tools/run_configs.sh || exit 1
       else TAG=$TAG/configs_$n bash tools/run_configs.sh || exit 1; fi ;;
