@@ -736,6 +736,50 @@ def main():
                         "buffer; PCIe-inclusive, not the headline value)"}
             del bufs
 
+    if args.mode == "schur" and not args.no_secondary and world == 1:
+        # One trust-region step's front end on the device, two ways
+        # (VERDICT r5 #6): the evaluation writes the gradient (gradient_mode
+        # 0, CameraGradientKernel) and cse_schur_init follows, or the
+        # evaluation skips the gradient and cse_schur_init_gradient forms
+        # g = J^T r from the same pass over J.  b = -r is refreshed from the
+        # evaluation's residuals in both, as the minimizer would.
+        ks = max(args.secondary_steps // 4, 10)
+        gvec = torch.empty(ne, dtype=f64, device=dev)
+
+        def with_gradient():
+            se.evaluate(residuals=True, jacobian=True, gradient=True)
+            torch.neg(se.residuals, out=bvec)
+            ev.schur_init_device(se.jacobian.data_ptr(), dvec.data_ptr(), bvec.data_ptr(),
+                                 srhs.data_ptr(), ca._cse.SCHUR_JACOBI)
+
+        def init_gradient():
+            se.evaluate(residuals=True, jacobian=True, gradient=False)
+            torch.neg(se.residuals, out=bvec)
+            ev.schur_init_gradient_device(se.jacobian.data_ptr(), dvec.data_ptr(), bvec.data_ptr(),
+                                          srhs.data_ptr(), gvec.data_ptr(), ca._cse.SCHUR_JACOBI)
+
+        def init_only():
+            ev.schur_init_device(se.jacobian.data_ptr(), dvec.data_ptr(), bvec.data_ptr(),
+                                 srhs.data_ptr(), ca._cse.SCHUR_JACOBI)
+
+        def init_gradient_only():
+            ev.schur_init_gradient_device(se.jacobian.data_ptr(), dvec.data_ptr(), bvec.data_ptr(),
+                                          srhs.data_ptr(), gvec.data_ptr(), ca._cse.SCHUR_JACOBI)
+
+        for name, fn, what in (
+                ("eval_gradient_then_init", with_gradient,
+                 "evaluation with gradient (gradient_mode 0) + b = -r + cse_schur_init"),
+                ("eval_then_init_gradient", init_gradient,
+                 "evaluation without gradient + b = -r + cse_schur_init_gradient (g from the "
+                 "init's pass over J)"),
+                ("init", init_only, "cse_schur_init alone"),
+                ("init_gradient", init_gradient_only, "cse_schur_init_gradient alone")):
+            for _ in range(3):
+                fn()
+            e, _, _ = run_leg(fn, ks, 0)
+            secondary[name] = {"value": ks / e, "unit": "steps/s", "ms_per_step": e / ks * 1e3,
+                               "steps": ks, "what": what}
+
     out = None
     if rank == 0:
         cpu = None

@@ -158,6 +158,8 @@ SIGNATURES = {
     "cse_schur_structure": (C.c_int, [C.c_void_p, P_i64, P_i64]),
     "cse_schur_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_int]),
+    "cse_schur_init_gradient": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_int, C.c_void_p]),
     "cse_schur_multiply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_schur_precondition": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cse_schur_back_substitute": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

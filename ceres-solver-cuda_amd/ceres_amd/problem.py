@@ -629,6 +629,15 @@ class Evaluator:
         return _cse.check(_cse.lib().cse_schur_init(self.handle, d_jacobian, d_D, d_b, d_rhs,
                                                     int(preconditioner)), "cse_schur_init")
 
+    def schur_init_gradient_device(self, d_jacobian, d_D, d_b, d_rhs, d_gradient,
+                                   preconditioner=_cse.SCHUR_JACOBI):
+        """schur_init_device plus the gradient g = J^T r (r = -b) into
+        d_gradient, in the same pass (cse_schur_init_gradient)."""
+        return _cse.check(_cse.lib().cse_schur_init_gradient(self.handle, d_jacobian, d_D, d_b,
+                                                             d_rhs, int(preconditioner),
+                                                             d_gradient),
+                          "cse_schur_init_gradient")
+
     def schur_multiply_device(self, d_x, d_y):
         """y = S x (ImplicitSchurComplement::RightMultiplyAndAccumulate)."""
         return _cse.check(_cse.lib().cse_schur_multiply(self.handle, d_x, d_y),

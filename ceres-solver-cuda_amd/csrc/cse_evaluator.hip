@@ -562,7 +562,7 @@ struct cse_evaluator {
     int64_t f_col_base = 0;   // f index of camera id = f_col_base + 9 id
     int64_t nchunks = 0, nbig = 0;
     DevBuf<int64_t> chunk_begin, big;
-    DevBuf<double> ete_inv, precond, partial;
+    DevBuf<double> ete_inv, precond, partial, gpartial;
     bool ready = false;
     int preconditioner = CSE_SCHUR_IDENTITY;
     const double *jac = nullptr, *D = nullptr, *b = nullptr;
@@ -2014,14 +2014,14 @@ cse::SchurArgs MakeSchurArgs(cse_evaluator* ev, const double* x, double* y) {
   return a;
 }
 
-template <int kMode>
+template <int kMode, bool kGrad = false>
 void LaunchSchurPass(const cse::SchurArgs& a, hipStream_t s) {
   constexpr int W = kOperatorWavesPerWg;
   if (a.nchunks > 0)
-    hipLaunchKernelGGL((cse::SchurChunkKernel<9, kMode, W>), dim3((unsigned)((a.nchunks + W - 1) / W)),
+    hipLaunchKernelGGL((cse::SchurChunkKernel<9, kMode, W, kGrad>), dim3((unsigned)((a.nchunks + W - 1) / W)),
                        dim3(W * cse::kWave), 0, s, a);
   if (a.nbig > 0)
-    hipLaunchKernelGGL((cse::SchurBigKernel<9, kMode>),
+    hipLaunchKernelGGL((cse::SchurBigKernel<9, kMode, kGrad>),
                        dim3((unsigned)((a.nbig + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
                        dim3(cse::kBlockThreads), 0, s, a);
 }
@@ -2044,6 +2044,36 @@ int SchurFTail(cse_evaluator* ev, double* y, hipStream_t s) {
   hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>),
                      dim3((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                      dim3(cse::kBlockThreads), 0, s, ga, ch);
+  CSE_HIP(hipGetLastError());
+  return CSE_OK;
+}
+
+// Init with the gradient: the contribution records hold F^T u and -F^T b;
+// one pass sums both per f block (GradientContribPairKernel), then the two
+// ordered reduces write rhs (f-vector indices) and the gradient's f rows.
+int SchurFTailWithGradient(cse_evaluator* ev, double* rhs, double* grad, hipStream_t s) {
+  const Group& G = ev->groups[0];
+  const Group::GradPlan& P = G.grad[0];
+  auto& S = ev->schur;
+  int rc;
+  if ((rc = S.gpartial.ensure((size_t)std::max<int64_t>(1, P.nchunks) * 9))) return rc;
+  const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
+  const cse::GradChunks chg{P.chunk_begin.p, P.chunk_off.p, S.gpartial.p, P.nchunks};
+  if (P.nchunks > 0)
+    hipLaunchKernelGGL((cse::GradientContribPairKernel<9, 10>),
+                       dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
+                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch, S.gpartial.p,
+                       P.chunk_order.p);
+  cse::GradArgs ga{};
+  ga.count = P.count;
+  ga.lo = P.lo;
+  ga.grad = rhs;
+  ga.delta_base = S.f_col_base;
+  const dim3 grid((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads));
+  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), grid, dim3(cse::kBlockThreads), 0, s, ga, ch);
+  ga.grad = grad;
+  ga.delta_base = G.delta_base[0];
+  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), grid, dim3(cse::kBlockThreads), 0, s, ga, chg);
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }
@@ -2071,8 +2101,10 @@ int cse_schur_structure(cse_evaluator* ev, int64_t* num_cols_e, int64_t* num_col
   return CSE_OK;
 }
 
-int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
-                   const double* d_b, double* d_rhs, int preconditioner) {
+extern "C++" {
+namespace {
+int SchurInit(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D, const double* d_b,
+              double* d_rhs, int preconditioner, double* d_gradient) {
   int rc = SchurCheck(ev, false);
   if (rc) return rc;
   if (!d_jacobian_values || !d_b || !d_rhs) return Fail(CSE_ERR_INVALID, "null pointer");
@@ -2086,7 +2118,7 @@ int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const dou
   Group& G = ev->groups[0];
   hipStream_t s = ev->stream;
   if ((rc = S.ete_inv.ensure((size_t)2 * S.e_cols))) return rc;
-  if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;
+  if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride * (d_gradient ? 2 : 1)))) return rc;
   S.jac = d_jacobian_values;
   S.D = d_D;
   S.b = d_b;
@@ -2096,9 +2128,18 @@ int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const dou
   CSE_HIP(hipMemsetAsync(ev->status.p + 1, 0, sizeof(int), s));
   CSE_HIP(hipMemsetAsync(d_rhs, 0, S.f_cols * sizeof(double), s));
   cse::SchurArgs a = MakeSchurArgs(ev, nullptr, nullptr);
-  LaunchSchurPass<cse::kSchurInit>(a, s);
-  CSE_HIP(hipGetLastError());
-  if ((rc = SchurFTail(ev, d_rhs, s))) return rc;
+  if (d_gradient) {
+    // Rows of blocks without residual blocks stay 0.
+    CSE_HIP(hipMemsetAsync(d_gradient, 0, ev->num_effective * sizeof(double), s));
+    a.grad = d_gradient;
+    LaunchSchurPass<cse::kSchurInit, true>(a, s);
+    CSE_HIP(hipGetLastError());
+    if ((rc = SchurFTailWithGradient(ev, d_rhs, d_gradient, s))) return rc;
+  } else {
+    LaunchSchurPass<cse::kSchurInit>(a, s);
+    CSE_HIP(hipGetLastError());
+    if ((rc = SchurFTail(ev, d_rhs, s))) return rc;
+  }
   if (preconditioner != CSE_SCHUR_IDENTITY) {
     const Group::GradPlan& P = G.grad[0];
     constexpr int T = cse::SymCount<9>();
@@ -2122,6 +2163,20 @@ int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const dou
   }
   S.ready = true;
   return CSE_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                   const double* d_b, double* d_rhs, int preconditioner) {
+  return SchurInit(ev, d_jacobian_values, d_D, d_b, d_rhs, preconditioner, nullptr);
+}
+
+int cse_schur_init_gradient(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                            const double* d_b, double* d_rhs, int preconditioner,
+                            double* d_gradient) {
+  if (!d_gradient) return Fail(CSE_ERR_INVALID, "null gradient");
+  return SchurInit(ev, d_jacobian_values, d_D, d_b, d_rhs, preconditioner, d_gradient);
 }
 
 int cse_schur_multiply(cse_evaluator* ev, const double* d_x, double* d_y) {

@@ -47,7 +47,8 @@ struct SchurArgs {
   int64_t b_base;
   const double* x;         // f vector (multiply, back substitution)
   double* ete_inv;         // M_p, packed upper triangle, at ete_inv + 2 * (e column of p)
-  double* contrib;         // [n][S0p] F_b^T u_b
+  double* contrib;         // [n][S0p] F_b^T u_b; init with the gradient: [n][2 S0p], then -F_b^T b_b
+  double* grad;            // init with the gradient: the e rows of g = J^T r = -J^T b
   double* y;               // back substitution: the full solution (e part written)
   const int64_t* chunk_begin;  // [nchunks][2] begin, end: wave chunks of whole e-block runs
   int64_t nchunks;
@@ -164,19 +165,30 @@ __device__ __forceinline__ void SchurEProducts(const double* E, const double* z,
   A[5] = E[2] * E[2] + E[5] * E[5];
 }
 
-// u_b = z_b - E_b w, then F_b^T u_b (S0 values, padded to S0p) to contrib.
-template <int S0>
+// u_b = z_b - E_b w, then F_b^T u_b (S0 values, padded to S0p) to contrib;
+// kGrad (init with the gradient): also -F_b^T z_b, the block's camera rows
+// of g = J^T r with z = b = -r, after them in a 2 S0p record.
+template <int S0, bool kGrad = false>
 __device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, const double* F,
                                              const double* E, const double* z, const double* w) {
   constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kRec = kGrad ? 2 * S0p : S0p;
   const double u0 = z[0] - (E[0] * w[0] + E[1] * w[1] + E[2] * w[2]);
   const double u1 = z[1] - (E[3] * w[0] + E[4] * w[1] + E[5] * w[2]);
-  double2* dst = reinterpret_cast<double2*>(a.contrib + (int64_t)S0p * i);
+  double2* dst = reinterpret_cast<double2*>(a.contrib + (int64_t)kRec * i);
 #pragma unroll
   for (int k = 0; k < S0p / 2; ++k) {
     const double c0 = F[2 * k] * u0 + F[S0 + 2 * k] * u1;
     const double c1 = 2 * k + 1 < S0 ? F[2 * k + 1] * u0 + F[S0 + 2 * k + 1] * u1 : 0.0;
     dst[k] = make_double2(c0, c1);
+  }
+  if constexpr (kGrad) {
+#pragma unroll
+    for (int k = 0; k < S0p / 2; ++k) {
+      const double c0 = -(F[2 * k] * z[0] + F[S0 + 2 * k] * z[1]);
+      const double c1 = 2 * k + 1 < S0 ? -(F[2 * k + 1] * z[0] + F[S0 + 2 * k + 1] * z[1]) : 0.0;
+      dst[S0p / 2 + k] = make_double2(c0, c1);
+    }
   }
 }
 
@@ -186,12 +198,17 @@ __device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, cons
 // lane reads its block's cells from LDS.  The contributions F_b^T u_b are
 // staged through the same LDS and leave as contiguous 16-byte pieces.
 // kWPB: waves per workgroup (chunk = workgroup * kWPB + wave).
-template <int S0, int kMode, int kWPB = kWavesPerBlock>
+// kGrad (kSchurInit only): also the gradient g = J^T r = -J^T b, its e rows
+// written here (-E^T b per e block) and its f rows' per-block parts staged
+// after the contributions (SchurContrib).
+template <int S0, int kMode, int kWPB = kWavesPerBlock, bool kGrad = false>
 __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs a) {
+  static_assert(!kGrad || kMode == kSchurInit, "the gradient comes with the init pass");
   constexpr int S0p = (S0 + 1) & ~1;
+  constexpr int kRec = kGrad ? 2 * S0p : S0p;  // doubles per contribution record
   constexpr int kF = 2 * S0;                // doubles per F cell
   constexpr int kImg = kWave * (kF + 6);    // F cells, then E cells, of up to a wave of blocks
-  static_assert(kF % 2 == 0 && kWave * S0p <= kImg, "16-byte pieces; contributions fit");
+  static_assert(kF % 2 == 0 && kWave * kRec <= kImg, "16-byte pieces; contributions fit");
   __shared__ double img_all[kWPB][kImg];
   const int lane = threadIdx.x & (kWave - 1), wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
   const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
@@ -276,6 +293,12 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
 #pragma unroll
   for (int k = 0; k < 3; ++k) s[k] = __shfl(s[k], e, kWave);
   const int64_t ecol = a.e_col_base + 3LL * id1;
+  if constexpr (kGrad) {  // the e block's gradient rows, -E^T b
+    if (active && lane == e) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.grad[ecol + k] = -s[k];
+    }
+  }
   double M[6];
   if constexpr (kMode == kSchurInit) {
 #pragma unroll
@@ -320,14 +343,22 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
     for (int k = 0; k < S0p / 2; ++k) {
       const double c0 = F[2 * k] * u0 + F[S0 + 2 * k] * u1;
       const double c1 = 2 * k + 1 < S0 ? F[2 * k + 1] * u0 + F[S0 + 2 * k + 1] * u1 : 0.0;
-      reinterpret_cast<double2*>(im + S0p * lane)[k] = make_double2(c0, c1);
+      reinterpret_cast<double2*>(im + kRec * lane)[k] = make_double2(c0, c1);
+    }
+    if constexpr (kGrad) {  // -F_b^T b_b after them
+#pragma unroll
+      for (int k = 0; k < S0p / 2; ++k) {
+        const double c0 = -(F[2 * k] * z[0] + F[S0 + 2 * k] * z[1]);
+        const double c1 = 2 * k + 1 < S0 ? -(F[2 * k + 1] * z[0] + F[S0 + 2 * k + 1] * z[1]) : 0.0;
+        reinterpret_cast<double2*>(im + kRec * lane)[S0p / 2 + k] = make_double2(c0, c1);
+      }
     }
     __builtin_amdgcn_wave_barrier();
     typedef double v2d __attribute__((ext_vector_type(2)));
-    v2d* dst = reinterpret_cast<v2d*>(a.contrib + (int64_t)S0p * i0);
-    const int pc = (S0p / 2) * nb;
+    v2d* dst = reinterpret_cast<v2d*>(a.contrib + (int64_t)kRec * i0);
+    const int pc = (kRec / 2) * nb;
 #pragma unroll
-    for (int k = 0; k < S0p / 2; ++k) {
+    for (int k = 0; k < kRec / 2; ++k) {
       const int p = k * kWave + lane;
       if (p < pc) __builtin_nontemporal_store(reinterpret_cast<const v2d*>(im)[p], dst + p);
     }
@@ -336,7 +367,7 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
 
 // One wave per e block with more rows than a wave: the rows are walked
 // twice, once for the sums and once for the contributions.
-template <int S0, int kMode>
+template <int S0, int kMode, bool kGrad = false>
 __global__ __launch_bounds__(kBlockThreads) void SchurBigKernel(const SchurArgs a) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t q = (int64_t)blockIdx.x * kWavesPerBlock + wave;
@@ -366,6 +397,12 @@ __global__ __launch_bounds__(kBlockThreads) void SchurBigKernel(const SchurArgs 
     }
   }
   const int64_t ecol = a.e_col_base + 3LL * id1;
+  if constexpr (kGrad) {
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.grad[ecol + k] = -s[k];
+    }
+  }
   double M[6];
   if constexpr (kMode == kSchurInit) {
     double d[3] = {0.0, 0.0, 0.0};
@@ -396,7 +433,7 @@ __global__ __launch_bounds__(kBlockThreads) void SchurBigKernel(const SchurArgs 
       const int id0 = (int)reinterpret_cast<const long long*>(a.ids)[i];
       double F[2 * S0], E[6], z[2];
       SchurLoadBlock<S0, kMode>(a, i, id0, F, E, z);
-      SchurContrib<S0>(a, i, F, E, z, w);
+      SchurContrib<S0, kGrad>(a, i, F, E, z, w);
     }
   }
 }

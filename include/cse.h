@@ -31,7 +31,7 @@ extern "C" {
  *    shard-local state in cse_create_multi.
  * 3: cse_options.jacobian_form.
  * 4: user functor kinds (cse_register_functor, cse_functor_shape),
- *    CSE_LOSS_USER and cse_loss.user. */
+ *    CSE_LOSS_USER and cse_loss.user, cse_schur_init_gradient. */
 #define CSE_ABI_VERSION 4
 
 /* Return codes. */
@@ -431,6 +431,19 @@ int cse_schur_structure(cse_evaluator* ev, int64_t* num_cols_e, int64_t* num_col
  * CSE_EVALUATION_FAILED, where Eigen's LLT would spread NaN silently. */
 int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
                    const double* d_b, double* d_rhs, int preconditioner);
+
+/* cse_schur_init, and also the gradient g = J^T r of the bound Jacobian into
+ * d_gradient (num_effective_parameters entries, assigned), taking r = -b --
+ * the trust-region step's b (TrustRegionMinimizer::EvaluateGradientAndJacobian
+ * evaluates g = J^T r beside J, trust_region_minimizer.cc:242-255) -- in the
+ * same pass over J: the e rows from the E^T b sums the init forms anyway,
+ * the f rows from a second half of each block's contribution record.  Then
+ * the evaluation before it needs no gradient (no CameraGradientKernel).
+ * Deterministic; equals the evaluation's gradient (gradient_mode 0) to
+ * rounding (a different summation order). */
+int cse_schur_init_gradient(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
+                            const double* d_b, double* d_rhs, int preconditioner,
+                            double* d_gradient);
 
 /* y = S x (ImplicitSchurComplement::RightMultiplyAndAccumulate, :101-141,
  * which assigns y); x and y have num_cols_f entries. */

@@ -21,7 +21,7 @@ import pytest
 import ceres_amd as ca
 from ceres_amd import bal
 import oracle_py as O
-from parity_util import assert_parity, is_approx
+from parity_util import COST_RTOL, assert_parity, is_approx
 
 pytestmark = pytest.mark.gpu
 
@@ -103,6 +103,19 @@ def test_problem_1778_compressed_row_huber(gpu):
                   report=rep_ng)
     print("problem-1778 CRS Huber parity:", rep)
     print("problem-1778 CRS Huber parity, residual+Jacobian kernel:", rep_ng)
+    del got, got_ng
+    # The Jet<double, 12> form of the CRS kernel at full size
+    # (cse_options.jacobian_form = CSE_JACOBIAN_JET: EvaluateAffineChunks
+    # TwoRoundCrsW1<SnavelyJetKind, ...>), against the same oracle values.
+    ev = ca.Evaluator(prog, jacobian_form="jet")
+    try:
+        got_jet = ev.evaluate(residuals=True, gradient=False, jacobian=True)
+    finally:
+        ev.close()
+    rep_jet = {}
+    assert_parity(drop_gradient(got_jet), drop_gradient(ref), "problem-1778 CRS Jet form",
+                  report=rep_jet)
+    print("problem-1778 CRS Huber parity, Jet<12> residual+Jacobian kernel:", rep_jet)
 
 
 @pytest.mark.parametrize("combo", range(8))
@@ -403,8 +416,10 @@ def test_problem_13682_full_size(gpu):
     assert prog.num_jacobian_values == 24 * O_
     # The gradient comes from the fused deterministic path (gradient_mode 0),
     # as in a trust-region Jacobian evaluation; then the headline evaluation
-    # bench.py times (residuals and Jacobian, no gradient:
-    # EvaluateAffineChunksTwoRoundW1 over all 28,987,644 blocks), as
+    # bench.py times (residuals and Jacobian, no gradient: the group-store
+    # kernel EvaluateAffineChunksGroupStore where GroupStoreEligible holds for
+    # the output strips, else EvaluateAffineChunksTwoRoundW1; 28,987,644
+    # blocks either way), as
     # TrustRegionMinimizer issues it at an accepted point
     # (trust_region_minimizer.cc:822-826).
     ev = ca.Evaluator(prog)
@@ -435,6 +450,22 @@ def test_problem_13682_full_size(gpu):
     assert_parity(drop_gradient(got_jet), drop_gradient(ref), "problem-13682 Jet form",
                   report=rep_jet)
     print("problem-13682 BSM Huber parity, Jet<12> residual+Jacobian kernel:", rep_jet)
+    del got_jet
+    # Residuals + cost only at full size (bench.py secondary.residual_only),
+    # and the cost alone, as ComputeCandidatePointAndEvaluateCost asks for
+    # the trust-region candidate (trust_region_minimizer.cc:770-787).
+    ev = ca.Evaluator(prog)
+    try:
+        ok, cost, r, g, j = ev.evaluate(residuals=True, gradient=False, jacobian=False)
+        ok_c, cost_c, *_ = ev.evaluate(residuals=False, gradient=False, jacobian=False)
+    finally:
+        ev.close()
+    assert ok_c and abs(cost_c - ref[1]) <= COST_RTOL * abs(ref[1])
+    assert g is None and j is None
+    rep_res = {}
+    assert_parity((ok, cost, r, None, None), (ref[0], ref[1], ref[2], None, None),
+                  "problem-13682 residual only", report=rep_res)
+    print("problem-13682 BSM Huber parity, residual-only kernel:", rep_res)
 
 
 def test_gradient_post_pass_deterministic_and_agrees_with_atomics(gpu):

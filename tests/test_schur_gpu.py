@@ -191,3 +191,86 @@ def test_schur_init_reports_singular_blocks_without_D(gpu):
                          _cse.SCHUR_JACOBI)
     assert ev.wait() == _cse.CSE_OK
     ev.close()
+
+
+@pytest.mark.parametrize("which", ["bal", "runs", "quaternion", "large"])
+@pytest.mark.parametrize("with_D", [True, False])
+def test_schur_init_gradient_equals_evaluation_gradient(gpu, which, with_D):
+    """cse_schur_init_gradient: the init also writes
+    g = J^T r (r = -b) -- what TrustRegionMinimizer::EvaluateGradientAndJacobian
+    (trust_region_minimizer.cc:242-255) gets from the evaluator beside J --
+    so the evaluation before it can skip its gradient.  g equals the
+    evaluation's gradient (gradient_mode 0) to 1e-13 relative, per entry
+    scaled by the gradient's max; rhs equals plain cse_schur_init's."""
+    if which == "runs":
+        prog = runs_problem()
+    elif which == "large":
+        prog = bal.synthetic_program((64, 20000, 90000), loss=ca.Loss.cauchy(2.0), seed=11)
+    else:
+        prog = bal.synthetic_program((10, 300, 1500), loss=ca.Loss.huber(1.0), seed=9,
+                                     quaternion_manifold=which == "quaternion")
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
+    ok, cost, r, g, jv = ev.evaluate()
+    assert ok
+    n = prog.num_effective_parameters
+    e_cols, f_cols = ev.schur_structure()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dj, db = t(jv), t(-r)
+    dD = t(np.random.default_rng(2).uniform(0.1, 2.0, n)) if with_D else None
+    D_ptr = dD.data_ptr() if with_D else None
+    rhs0 = torch.empty(f_cols, dtype=torch.float64, device=dev)
+    rhs1 = torch.full((f_cols,), np.nan, dtype=torch.float64, device=dev)
+    dg = torch.full((n,), np.nan, dtype=torch.float64, device=dev)
+    ev.schur_init_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs0.data_ptr(), _cse.SCHUR_JACOBI)
+    rc0 = ev.wait()
+    ev.schur_init_gradient_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs1.data_ptr(),
+                                  dg.data_ptr(), _cse.SCHUR_JACOBI)
+    rc1 = ev.wait()
+    # without D the runs problem has singular point blocks: both inits say so
+    assert rc0 == rc1
+    got = dg.cpu().numpy()
+    assert np.isfinite(got).all()
+    scale = np.abs(g).max()
+    assert np.abs(got - g).max() <= 1e-13 * scale
+    assert close(got, g, 1e-13)
+    a, b_ = rhs1.cpu().numpy(), rhs0.cpu().numpy()
+    assert np.abs(a - b_).max() <= 1e-13 * np.abs(b_).max()
+    # the gradient written here drives the next init too: a second call is
+    # bit-identical (fixed-order sums)
+    dg2 = torch.empty_like(dg)
+    ev.schur_init_gradient_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs1.data_ptr(),
+                                  dg2.data_ptr(), _cse.SCHUR_JACOBI)
+    ev.wait()
+    assert torch.equal(dg, dg2)
+    ev.close()
+
+
+def test_schur_init_gradient_after_gradient_free_evaluation(gpu):
+    """The intended sequence: cse_evaluate_device without a gradient pointer
+    (no CameraGradientKernel), then cse_schur_init_gradient with b = -r; the
+    gradient equals a full evaluation's."""
+    prog = bal.synthetic_program((32, 4000, 20000), loss=ca.Loss.huber(1.0), seed=5)
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
+    ok, cost, r, g, jv = ev.evaluate()
+    assert ok
+    n, m = prog.num_effective_parameters, prog.num_residuals
+    e_cols, f_cols = ev.schur_structure()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dx = t(prog.state)
+    dcost = torch.empty(1, dtype=torch.float64, device=dev)
+    dr = torch.empty(m, dtype=torch.float64, device=dev)
+    dj = torch.empty(prog.num_jacobian_values, dtype=torch.float64, device=dev)
+    ev.evaluate_device(dx.data_ptr(), dcost.data_ptr(), dr.data_ptr(), None, dj.data_ptr())
+    assert ev.wait() == _cse.CSE_OK
+    db = -dr
+    dD = t(np.full(n, 0.25))
+    rhs = torch.empty(f_cols, dtype=torch.float64, device=dev)
+    dg = torch.empty(n, dtype=torch.float64, device=dev)
+    ev.schur_init_gradient_device(dj.data_ptr(), dD.data_ptr(), db.data_ptr(), rhs.data_ptr(),
+                                  dg.data_ptr(), _cse.SCHUR_JACOBI)
+    assert ev.wait() == _cse.CSE_OK
+    got = dg.cpu().numpy()
+    assert np.abs(got - g).max() <= 1e-13 * np.abs(g).max()
+    ev.close()
