@@ -780,6 +780,20 @@ def main():
             secondary[name] = {"value": ks / e, "unit": "steps/s", "ms_per_step": e / ks * 1e3,
                                "steps": ks, "what": what}
 
+    # Every rank's block range, gathered (the shard cuts of
+    # shard.point_bucket_cuts as each rank built them): they must tile
+    # [0, observations) in rank order.
+    cuts = [0] * (2 * world)
+    cuts[2 * rank], cuts[2 * rank + 1] = se.shard.blocks
+    if world > 1:
+        ct = torch.tensor(cuts, dtype=torch.int64, device="cpu" if backend == "gloo" else dev)
+        dist.all_reduce(ct)
+        cuts = [int(v) for v in ct.cpu()]
+    block_cuts = cuts[0::2] + [cuts[-1]]
+    if strong and (block_cuts[0] != 0 or block_cuts[-1] != bal.CONFIGS[args.config][2] or
+                   any(cuts[2 * r + 1] != cuts[2 * r + 2] for r in range(world - 1))):
+        raise SystemExit(f"shard block ranges do not tile the problem: {cuts}")
+
     out = None
     if rank == 0:
         cpu = None
@@ -831,6 +845,7 @@ def main():
                             + f"{'+gradient' if args.gradient else ''}, device-resident",
                 "cameras": C_, "points": P_, "observations": O_,
                 "blocks_rank0": sh.blocks[1] - sh.blocks[0],
+                "block_cuts": block_cuts if strong else None,
                 "parallelism": (f"rank 0's shard of {args.shard_of} (one process)" if args.shard_of > 1
                                 else "single GPU" if world == 1 else
                                 f"point-bucket block sharding x{world}" if strong else

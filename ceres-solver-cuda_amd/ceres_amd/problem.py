@@ -375,6 +375,16 @@ class ProblemCUDA:
         ids = np.ascontiguousarray(np.asarray(ids, np.int32).reshape(-1, len(functor_shape(kind)[1])))
         data = np.ascontiguousarray(np.asarray(data, np.float64).reshape(ids.shape[0], -1))
         n = ids.shape[0]
+        if n and (ids.min() < 0 or ids.max() >= len(self._sizes)):
+            raise ValueError("add_residual_blocks: parameter block id out of range")
+        if n and ids.shape[1] > 1:
+            # ProblemImpl::AddResidualBlock (problem_impl.cc:285-301) refuses a
+            # parameter block listed twice in one residual block.
+            srt = np.sort(ids, axis=1)
+            dup = np.flatnonzero((srt[:, 1:] == srt[:, :-1]).any(axis=1))
+            if dup.size:
+                raise ValueError(f"add_residual_blocks: duplicate parameter blocks in residual "
+                                 f"block {self._nrb + int(dup[0])}: {ids[dup[0]].tolist()}")
         self._groups.append(ResidualGroup(kind, loss or Loss.trivial(), ids, data, None, self._nrb))
         self._nrb += n
         return range(self._nrb - n, self._nrb)

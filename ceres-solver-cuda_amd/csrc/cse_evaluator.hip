@@ -31,12 +31,14 @@
 #include "multi_device.h"
 #include "schur_kernels.hpp"
 
+namespace cse {
+std::string& LastError();  // layout.cpp: one per thread, shared by every entry point
+}  // namespace cse
+
 namespace {
 
-thread_local std::string g_last_error;
-
 int Fail(int code, const std::string& msg) {
-  g_last_error = msg;
+  cse::LastError() = msg;
   return code;
 }
 
@@ -1430,7 +1432,7 @@ void cse_default_options(cse_options* o) {
   o->apply_loss_function = 1;
 }
 
-const char* cse_last_error(void) { return g_last_error.c_str(); }
+const char* cse_last_error(void) { return cse::LastError().c_str(); }
 
 int cse_abi_version(void) { return CSE_ABI_VERSION; }
 

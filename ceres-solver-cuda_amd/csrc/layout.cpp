@@ -7,12 +7,27 @@
 //   BlockSparseMatrix           block_jacobian_writer.cc:62-160
 //   CompressedRowSparseMatrix   compressed_row_jacobian_writer.cc:93-193,240-300
 #include <algorithm>
+#include <string>
 #include <utility>
 #include <vector>
 
 #include "../../include/cse.h"
 
+namespace cse {
+// cse_last_error's text (cse_evaluator.hip), kept here so the layout
+// builders can set it when they are linked without the evaluator.
+std::string& LastError() {
+  thread_local std::string text;
+  return text;
+}
+}  // namespace cse
+
 namespace {
+
+int Invalid(const std::string& msg) {
+  cse::LastError() = msg;
+  return CSE_ERR_INVALID;
+}
 
 bool Active(const cse_parameter_block* pbs, int32_t id) { return !pbs[id].is_constant; }
 
@@ -44,7 +59,8 @@ extern "C" int cse_block_sparse_layout(int64_t npb, const cse_parameter_block* p
                                        int64_t* residual_layout, int64_t* per_residual_layout,
                                        int64_t* per_residual_offsets,
                                        int64_t* num_jacobian_values) {
-  if (npb < 0 || nrb < 0 || !param_begin || !nres || !residual_layout) return CSE_ERR_INVALID;
+  if (npb < 0 || nrb < 0 || !param_begin || !nres || !residual_layout)
+    return Invalid("layout: negative count or missing table");
   const std::vector<int64_t> index = ActiveIndex(npb, pbs);
   auto is_e = [&](int32_t id) { return index[id] < num_eliminate_blocks; };
   // Pass 1: the E cells occupy [0, e_total); F cells follow.
@@ -83,7 +99,8 @@ extern "C" int cse_compressed_row_layout(int64_t npb, const cse_parameter_block*
                                          int64_t* per_residual_offsets,
                                          int64_t* num_jacobian_values, int64_t* crs_rows,
                                          int64_t* crs_cols) {
-  if (npb < 0 || nrb < 0 || !param_begin || !nres || !residual_layout) return CSE_ERR_INVALID;
+  if (npb < 0 || nrb < 0 || !param_begin || !nres || !residual_layout)
+    return Invalid("layout: negative count or missing table");
   const std::vector<int64_t> index = ActiveIndex(npb, pbs);
   int64_t row = 0, value = 0, t = 0;
   if (crs_rows) crs_rows[0] = 0;
@@ -105,7 +122,9 @@ extern "C" int cse_compressed_row_layout(int64_t npb, const cse_parameter_block*
     }
     std::sort(order.begin(), order.end());
     for (size_t m = 1; m < order.size(); ++m)
-      if (order[m].first == order[m - 1].first) return CSE_ERR_INVALID;  // duplicate block
+      if (order[m].first == order[m - 1].first)
+        return Invalid("layout: residual block " + std::to_string(i) +
+                       " lists a parameter block twice");
     // Map active argument -> parameter block id.
     order_id.assign(order.size(), -1);
     {

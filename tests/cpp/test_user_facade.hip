@@ -189,7 +189,16 @@ static void BundlerWithUserLoss(JacobianFormat format) {
       J(evaluator.NumJacobianValues());
   EXPECT(evaluator.Evaluate(state.data(), &cost, r.data(), g.data(), J.data()));
 
-  // Oracle: program order points then cameras, residual blocks in insertion order.
+  // Oracle: program order = the elimination group (points), then the
+  // cameras in the order AddResidualBlock first saw them (ProblemImpl adds
+  // a block at first use), residual blocks in insertion order.
+  std::vector<int> cam_pos(nc, -1), cam_order;
+  for (const Obs& o : obs)
+    if (cam_pos[o.c] < 0) {
+      cam_pos[o.c] = (int)cam_order.size();
+      cam_order.push_back(o.c);
+    }
+  EXPECT((int)cam_order.size() == nc);
   const int npb = np + nc;
   std::vector<int32_t> pb_size(npb), pb_const(npb, 0), kind(nrb, ORACLE_BUNDLER_RESIDUAL_2_9_3);
   std::vector<int64_t> pb_pj(npb, -1);
@@ -201,7 +210,7 @@ static void BundlerWithUserLoss(JacobianFormat format) {
   for (int i = 0; i < nrb; ++i) {
     lsd[i] = i % 2;
     ls[i] = i % 2 ? 0.5 : 1.0;
-    params[2 * i] = np + obs[i].c;
+    params[2 * i] = np + cam_pos[obs[i].c];
     params[2 * i + 1] = obs[i].p;
     data[2 * i] = obs[i].u;
     data[2 * i + 1] = obs[i].v;
@@ -217,7 +226,7 @@ static void BundlerWithUserLoss(JacobianFormat format) {
   EXPECT(oracle_sizes_of(&p, &sz) == 0);
   EXPECT(sz.num_jacobian_values == evaluator.NumJacobianValues());
   std::vector<double> ostate(pts);
-  ostate.insert(ostate.end(), cams.begin(), cams.end());
+  for (int c : cam_order) ostate.insert(ostate.end(), &cams[9 * c], &cams[9 * c] + 9);
   EXPECT(ostate == state);
   double ocost = -1;
   std::vector<double> orr(2 * nrb), og(sz.num_effective_parameters), oJ(sz.num_jacobian_values);

@@ -138,8 +138,10 @@ def test_general_path_functors_equal_library_test_kinds(gpu):
     xs = [pb.add_parameter_block(rng.normal(size=2)) for _ in range(40)]
     ones = [pb.add_parameter_block(rng.normal(size=1)) for _ in range(30)]
     n = 500
-    bil = np.stack([rng.choice(xs, n), rng.choice(xs, n)], axis=1)
-    ten = np.stack([rng.choice(ones, n, replace=True) for _ in range(10)], axis=1)
+    # distinct blocks within each residual block (ProblemImpl::AddResidualBlock
+    # refuses a block listed twice, problem_impl.cc:285-301)
+    bil = np.stack([rng.choice(xs, 2, replace=False) for _ in range(n)])
+    ten = np.stack([rng.choice(ones, 10, replace=False) for _ in range(n)])
     pb.add_residual_blocks(_cse.TEST_BILINEAR_1_2_2, None, bil, rng.normal(size=(n, 1)))
     pb.add_residual_blocks(_cse.TEST_TEN_PARAMETER_1_x10, None, ten, np.zeros((n, 1)))
     lib_prog = pb.program()
