@@ -108,6 +108,10 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the gradient / residual-only / host-strip legs")
     ap.add_argument("--secondary-steps", type=int, default=20)
+    ap.add_argument("--settle", type=float, default=0.25,
+                    help="seconds of untimed steps before the --warmup steps (the clocks ramp "
+                         "over tens of ms after the idle problem build); reported as "
+                         "settle_steps")
     ap.add_argument("--host-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-only", action="store_true",
@@ -442,9 +446,21 @@ def main():
     f64 = torch.float64
     units = world if not strong else 1  # whole-problem evaluations per step
 
-    def run_leg(step, steps, warmup):
+    def run_leg(step, steps, warmup, settle_s=0.0):
         """Warm-up, then `steps` timed steps between barrier + synchronize;
-        returns (elapsed_s, kernel_ms_local, kernel_ms_max) maxed over ranks."""
+        returns (elapsed_s, kernel_ms_local, kernel_ms_max) maxed over ranks.
+        settle_s: before the `warmup` steps, untimed steps until that many
+        seconds have passed (the GPU's clocks ramp over tens of ms after the
+        idle problem build: profiles/round6/ramp)."""
+        t_s, n_s = time.perf_counter(), 0
+        while settle_s > 0:  # rounds of 8 steps; every rank runs the same count
+            for _ in range(8):
+                step()
+            n_s += 8
+            torch.cuda.synchronize(dev)
+            if reduce_max([time.perf_counter() - t_s])[0] >= settle_s:
+                break
+        settle[0] += n_s
         for _ in range(warmup):
             step()
         se.wait_exchange()
@@ -524,7 +540,9 @@ def main():
             ev.right_multiply_device(se.jacobian.data_ptr(), pvec.data_ptr(), jp.data_ptr())
             ev.left_multiply_device(se.jacobian.data_ptr(), jp.data_ptr(), jtjp.data_ptr())
 
-    elapsed, kernel_ms, kernel_ms_max = run_leg(step, args.steps, args.warmup)
+    settle = [0]
+    elapsed, kernel_ms, kernel_ms_max = run_leg(step, args.steps, args.warmup, args.settle)
+    settle_steps = settle[0]
     if args.mode in ("spmv", "cgnr", "schur"):  # no evaluate launches in the loop: the step time
         kernel_ms = kernel_ms_max = elapsed / args.steps * 1e3
 
@@ -824,6 +842,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": settle_steps,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": args.scaling,

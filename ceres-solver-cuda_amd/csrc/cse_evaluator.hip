@@ -564,7 +564,7 @@ struct cse_evaluator {
     int64_t f_col_base = 0;   // f index of camera id = f_col_base + 9 id
     int64_t nchunks = 0, nbig = 0;
     DevBuf<int64_t> chunk_begin, big;
-    DevBuf<double> ete_inv, precond, partial, gpartial;
+    DevBuf<double> ete_inv, precond, partial, ub;
     bool ready = false;
     int preconditioner = CSE_SCHUR_IDENTITY;
     const double *jac = nullptr, *D = nullptr, *b = nullptr;
@@ -2050,34 +2050,30 @@ int SchurFTail(cse_evaluator* ev, double* y, hipStream_t s) {
   return CSE_OK;
 }
 
-// Init with the gradient: the contribution records hold F^T u and -F^T b;
-// one pass sums both per f block (GradientContribPairKernel), then the two
-// ordered reduces write rhs (f-vector indices) and the gradient's f rows.
-int SchurFTailWithGradient(cse_evaluator* ev, double* rhs, double* grad, hipStream_t s) {
-  const Group& G = ev->groups[0];
-  const Group::GradPlan& P = G.grad[0];
-  auto& S = ev->schur;
-  int rc;
-  if ((rc = S.gpartial.ensure((size_t)std::max<int64_t>(1, P.nchunks) * 9))) return rc;
-  const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
-  const cse::GradChunks chg{P.chunk_begin.p, P.chunk_off.p, S.gpartial.p, P.nchunks};
+// The init's camera-order pass and the per-camera finish (schur_kernels.hpp).
+struct SchurCameraLaunch {
+  cse::SchurArgs a;
+  const Group::GradPlan* P;
+  cse::GradChunks ch;
+  const double* D;
+  int64_t d_off;  // D index of the plan's first camera's first column
+  double* precond;
+  int* status;
+  double* rhs;   // rhs row of the plan's first camera
+  double* grad;  // gradient row of the plan's first camera (null: no gradient)
+};
+
+template <int kDiag, bool kGrad>
+void LaunchSchurCameraPass(const SchurCameraLaunch& L, hipStream_t s) {
+  const Group::GradPlan& P = *L.P;
   if (P.nchunks > 0)
-    hipLaunchKernelGGL((cse::GradientContribPairKernel<9, 10>),
+    hipLaunchKernelGGL((cse::SchurCameraPassKernel<9, kDiag, kGrad>),
                        dim3((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock)),
-                       dim3(cse::kBlockThreads), 0, s, G.gcontrib.p, P.perm.p, ch, S.gpartial.p,
-                       P.chunk_order.p);
-  cse::GradArgs ga{};
-  ga.count = P.count;
-  ga.lo = P.lo;
-  ga.grad = rhs;
-  ga.delta_base = S.f_col_base;
-  const dim3 grid((unsigned)((ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads));
-  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), grid, dim3(cse::kBlockThreads), 0, s, ga, ch);
-  ga.grad = grad;
-  ga.delta_base = G.delta_base[0];
-  hipLaunchKernelGGL((cse::GradientChunkReduceKernel<9>), grid, dim3(cse::kBlockThreads), 0, s, ga, chg);
-  CSE_HIP(hipGetLastError());
-  return CSE_OK;
+                       dim3(cse::kBlockThreads), 0, s, L.a, P.perm.p, L.ch, P.chunk_order.p);
+  if (P.count > 0)
+    hipLaunchKernelGGL((cse::SchurCameraFinishKernel<9, kDiag, kGrad>),
+                       dim3((unsigned)((P.count + 63) / 64)), dim3(64), 0, s, L.ch, P.count, L.D,
+                       L.d_off, L.precond, L.status, L.rhs, L.grad);
 }
 
 int SchurCheck(cse_evaluator* ev, bool need_ready) {
@@ -2119,50 +2115,51 @@ int SchurInit(cse_evaluator* ev, const double* d_jacobian_values, const double* 
                 "SCHUR_JACOBI: an e block sees one f block in two residual blocks");
   Group& G = ev->groups[0];
   hipStream_t s = ev->stream;
+  const bool grad = d_gradient != nullptr;
   if ((rc = S.ete_inv.ensure((size_t)2 * S.e_cols))) return rc;
-  if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride * (d_gradient ? 2 : 1)))) return rc;
+  if ((rc = G.gcontrib.ensure((size_t)G.n * G.slot0_stride))) return rc;  // the multiplies'
+  if ((rc = S.ub.ensure((size_t)G.n * (grad ? 4 : 2)))) return rc;
   S.jac = d_jacobian_values;
   S.D = d_D;
   S.b = d_b;
   S.preconditioner = preconditioner;
-  // M_p and rhs = F^T (b - E M E^T b).  The status word read by cse_wait
-  // reports a non-positive pivot (schur_kernels.hpp, PivotOk).
+  // Point order: M_p, u_b = b_b - E_b M_p E_b^T b (and the gradient's e
+  // rows); then camera order: rhs = F^T u, the gradient's f rows -F^T b and
+  // the preconditioner's F^T Q F, each F cell read once.  The status word
+  // read by cse_wait reports a non-positive pivot (schur_kernels.hpp, PivotOk).
   CSE_HIP(hipMemsetAsync(ev->status.p + 1, 0, sizeof(int), s));
   CSE_HIP(hipMemsetAsync(d_rhs, 0, S.f_cols * sizeof(double), s));
-  cse::SchurArgs a = MakeSchurArgs(ev, nullptr, nullptr);
-  if (d_gradient) {
-    // Rows of blocks without residual blocks stay 0.
+  if (grad)  // rows of blocks without residual blocks stay 0
     CSE_HIP(hipMemsetAsync(d_gradient, 0, ev->num_effective * sizeof(double), s));
-    a.grad = d_gradient;
+  cse::SchurArgs a = MakeSchurArgs(ev, nullptr, nullptr);
+  a.ub = S.ub.p;
+  a.grad = d_gradient;
+  if (grad)
     LaunchSchurPass<cse::kSchurInit, true>(a, s);
-    CSE_HIP(hipGetLastError());
-    if ((rc = SchurFTailWithGradient(ev, d_rhs, d_gradient, s))) return rc;
-  } else {
+  else
     LaunchSchurPass<cse::kSchurInit>(a, s);
-    CSE_HIP(hipGetLastError());
-    if ((rc = SchurFTail(ev, d_rhs, s))) return rc;
+  CSE_HIP(hipGetLastError());
+  const Group::GradPlan& P = G.grad[0];
+  const int diag = preconditioner == CSE_SCHUR_IDENTITY ? 0 : preconditioner == CSE_SCHUR_JACOBI ? 1 : 2;
+  const int parts = (diag ? cse::SymCount<9>() : 0) + 9 * (grad ? 2 : 1);
+  if ((rc = S.partial.ensure((size_t)std::max<int64_t>(1, P.nchunks) * parts))) return rc;
+  if (diag && (rc = S.precond.ensure((size_t)81 * P.count))) return rc;
+  const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, S.partial.p, P.nchunks};
+  // d_off: D index of camera lo + p = e_cols + f index = e_cols + f_col_base + 9 (lo + p).
+  const int64_t d_off = S.e_cols + S.f_col_base + 9LL * P.lo;
+  double* rhs_p = d_rhs + S.f_col_base + 9LL * P.lo;
+  double* grad_p = grad ? d_gradient + G.delta_base[0] + 9LL * P.lo : nullptr;
+  int* status = ev->status.p + 1;
+  const SchurCameraLaunch L{a, &P, ch, d_D, d_off, S.precond.p, status, rhs_p, grad_p};
+  switch (diag * 2 + (grad ? 1 : 0)) {
+    case 0: LaunchSchurCameraPass<0, false>(L, s); break;
+    case 1: LaunchSchurCameraPass<0, true>(L, s); break;
+    case 2: LaunchSchurCameraPass<1, false>(L, s); break;
+    case 3: LaunchSchurCameraPass<1, true>(L, s); break;
+    case 4: LaunchSchurCameraPass<2, false>(L, s); break;
+    default: LaunchSchurCameraPass<2, true>(L, s); break;
   }
-  if (preconditioner != CSE_SCHUR_IDENTITY) {
-    const Group::GradPlan& P = G.grad[0];
-    constexpr int T = cse::SymCount<9>();
-    if ((rc = S.partial.ensure((size_t)std::max<int64_t>(1, P.nchunks) * T))) return rc;
-    if ((rc = S.precond.ensure((size_t)81 * P.count))) return rc;
-    const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, S.partial.p, P.nchunks};
-    const dim3 grid((unsigned)((P.nchunks + cse::kWavesPerBlock - 1) / cse::kWavesPerBlock));
-    if (P.nchunks > 0) {
-      if (preconditioner == CSE_SCHUR_SCHUR_JACOBI)
-        hipLaunchKernelGGL((cse::SchurBlockDiagKernel<9, true>), grid, dim3(cse::kBlockThreads), 0,
-                           s, a, P.perm.p, ch);
-      else
-        hipLaunchKernelGGL((cse::SchurBlockDiagKernel<9, false>), grid, dim3(cse::kBlockThreads), 0,
-                           s, a, P.perm.p, ch);
-    }
-    // d_off: D index of camera lo + p = e_cols + f index = e_cols + f_col_base + 9 (lo + p).
-    hipLaunchKernelGGL((cse::SchurBlockInvertKernel<9>), dim3((unsigned)((P.count + 63) / 64)),
-                       dim3(64), 0, s, ch, P.count, d_D,
-                       S.e_cols + S.f_col_base + 9LL * P.lo, S.precond.p, ev->status.p + 1);
-    CSE_HIP(hipGetLastError());
-  }
+  CSE_HIP(hipGetLastError());
   S.ready = true;
   return CSE_OK;
 }

@@ -203,49 +203,6 @@ __global__ __launch_bounds__(kBlockThreads) void GradientContribKernel(const dou
   }
 }
 
-// The same over records of two SP halves (ImplicitSchurComplement::Init
-// with the gradient, SchurContrib<S0, true>): the first halves' sums into
-// ch.partial, the second halves' into partial2.
-template <int S, int SP>
-__global__ __launch_bounds__(kBlockThreads) void GradientContribPairKernel(const double* contrib,
-                                                                           const int32_t* perm,
-                                                                           const GradChunks ch,
-                                                                           double* partial2,
-                                                                           const int32_t* order) {
-  static_assert(SP % 2 == 0 && SP >= S, "16-byte records");
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int64_t slot = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  if (slot >= ch.nchunks) return;
-  const int64_t cid = order ? (int64_t)order[slot] : slot;
-  const int64_t q1 = ch.begin[cid + 1];
-  double acc[S], acc2[S];
-#pragma unroll
-  for (int c = 0; c < S; ++c) acc[c] = acc2[c] = 0.0;
-  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
-    const double2* rec = reinterpret_cast<const double2*>(contrib + (int64_t)(2 * SP) * perm[q]);
-#pragma unroll
-    for (int h = 0; h < SP / 2; ++h) {
-      const double2 v = rec[h], u = rec[SP / 2 + h];
-      if (2 * h < S) acc[2 * h] += v.x, acc2[2 * h] += u.x;
-      if (2 * h + 1 < S) acc[2 * h + 1] += v.y, acc2[2 * h + 1] += u.y;
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < S; ++c)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      acc[c] += __shfl_xor(acc[c], off, kWave);
-      acc2[c] += __shfl_xor(acc2[c], off, kWave);
-    }
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < S; ++c) {
-      ch.partial[cid * S + c] = acc[c];
-      partial2[cid * S + c] = acc2[c];
-    }
-  }
-}
-
 // Fused-gradient slot 1: the waves' boundary entries (sum[S], id) are in
 // wave order, so their ids are non-decreasing; the first entry of each id
 // adds that id's entries in order and adds the sum to the row (no interior

@@ -15,13 +15,16 @@
 // is S = F^T F + D_f^2 - F^T E M E^T F.  Every operation below is, per e
 // block p and its rows b:
 //     s_p = sum_b E_b^T z_b,   w_p = M_p s_p,   u_b = z_b - E_b w_p
-// followed by the f-block sum y_c += sum_{b of c} F_b^T u_b (the blocks'
-// F_b^T u_b are written in block order and summed per f block in a fixed
-// order by GradientContribKernel + GradientChunkReduceKernel, as the fused
-// gradient's camera rows), with
+// followed by the f-block sum y_c += sum_{b of c} F_b^T u_b, with
 //     init (UpdateRhs, implicit_schur_complement.cc:240-273):  z_b = b_b,
-//          and M_p computed and stored (AddDiagonalAndInvert, :190-214)
-//     multiply (RightMultiplyAndAccumulate, :101-141):  z_b = F_b x_c
+//          and M_p computed and stored (AddDiagonalAndInvert, :190-214);
+//          u_b (and b_b, for the gradient) are written per block and one
+//          camera-order pass (SchurCameraPassKernel) forms F^T u, F^T b and
+//          the preconditioner's F^T Q F together, reading each F cell once
+//     multiply (RightMultiplyAndAccumulate, :101-141):  z_b = F_b x_c, the
+//          blocks' F_b^T u_b written in block order and summed per f block
+//          in a fixed order by GradientContribKernel +
+//          GradientChunkReduceKernel, as the fused gradient's camera rows
 //     back substitution (BackSubstitute, :216-238):  z_b = b_b - F_b x_c,
 //          y_p = w_p, no f-block sum.
 // All sums run in a fixed order: results are bit-identical run to run.
@@ -47,7 +50,8 @@ struct SchurArgs {
   int64_t b_base;
   const double* x;         // f vector (multiply, back substitution)
   double* ete_inv;         // M_p, packed upper triangle, at ete_inv + 2 * (e column of p)
-  double* contrib;         // [n][S0p] F_b^T u_b; init with the gradient: [n][2 S0p], then -F_b^T b_b
+  double* contrib;         // multiply: [n][S0p] F_b^T u_b
+  double* ub;              // init: [n][2] u_b, or [n][4] u_b then b_b with the gradient
   double* grad;            // init with the gradient: the e rows of g = J^T r = -J^T b
   double* y;               // back substitution: the full solution (e part written)
   const int64_t* chunk_begin;  // [nchunks][2] begin, end: wave chunks of whole e-block runs
@@ -165,31 +169,31 @@ __device__ __forceinline__ void SchurEProducts(const double* E, const double* z,
   A[5] = E[2] * E[2] + E[5] * E[5];
 }
 
-// u_b = z_b - E_b w, then F_b^T u_b (S0 values, padded to S0p) to contrib;
-// kGrad (init with the gradient): also -F_b^T z_b, the block's camera rows
-// of g = J^T r with z = b = -r, after them in a 2 S0p record.
-template <int S0, bool kGrad = false>
+// u_b = z_b - E_b w, then F_b^T u_b (S0 values, padded to S0p) to contrib.
+template <int S0>
 __device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, const double* F,
                                              const double* E, const double* z, const double* w) {
   constexpr int S0p = (S0 + 1) & ~1;
-  constexpr int kRec = kGrad ? 2 * S0p : S0p;
   const double u0 = z[0] - (E[0] * w[0] + E[1] * w[1] + E[2] * w[2]);
   const double u1 = z[1] - (E[3] * w[0] + E[4] * w[1] + E[5] * w[2]);
-  double2* dst = reinterpret_cast<double2*>(a.contrib + (int64_t)kRec * i);
+  double2* dst = reinterpret_cast<double2*>(a.contrib + (int64_t)S0p * i);
 #pragma unroll
   for (int k = 0; k < S0p / 2; ++k) {
     const double c0 = F[2 * k] * u0 + F[S0 + 2 * k] * u1;
     const double c1 = 2 * k + 1 < S0 ? F[2 * k + 1] * u0 + F[S0 + 2 * k + 1] * u1 : 0.0;
     dst[k] = make_double2(c0, c1);
   }
-  if constexpr (kGrad) {
-#pragma unroll
-    for (int k = 0; k < S0p / 2; ++k) {
-      const double c0 = -(F[2 * k] * z[0] + F[S0 + 2 * k] * z[1]);
-      const double c1 = 2 * k + 1 < S0 ? -(F[2 * k + 1] * z[0] + F[S0 + 2 * k + 1] * z[1]) : 0.0;
-      dst[S0p / 2 + k] = make_double2(c0, c1);
-    }
-  }
+}
+
+// Init: block i's u_b (and b_b) record.
+template <bool kGrad>
+__device__ __forceinline__ void SchurStoreU(const SchurArgs& a, int64_t i, const double* E,
+                                            const double* z, const double* w) {
+  const double u0 = z[0] - (E[0] * w[0] + E[1] * w[1] + E[2] * w[2]);
+  const double u1 = z[1] - (E[3] * w[0] + E[4] * w[1] + E[5] * w[2]);
+  double2* dst = reinterpret_cast<double2*>(a.ub + (kGrad ? 4 : 2) * i);
+  dst[0] = make_double2(u0, u1);
+  if constexpr (kGrad) dst[1] = make_double2(z[0], z[1]);
 }
 
 // One wave per chunk of whole e-block runs.  The chunk's F cells and E cells
@@ -198,17 +202,21 @@ __device__ __forceinline__ void SchurContrib(const SchurArgs& a, int64_t i, cons
 // lane reads its block's cells from LDS.  The contributions F_b^T u_b are
 // staged through the same LDS and leave as contiguous 16-byte pieces.
 // kWPB: waves per workgroup (chunk = workgroup * kWPB + wave).
+// Init reads no F cell: it writes u_b per block for the camera pass.
 // kGrad (kSchurInit only): also the gradient g = J^T r = -J^T b, its e rows
-// written here (-E^T b per e block) and its f rows' per-block parts staged
-// after the contributions (SchurContrib).
+// written here (-E^T b per e block), b_b beside u_b for its f rows.
 template <int S0, int kMode, int kWPB = kWavesPerBlock, bool kGrad = false>
 __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs a) {
   static_assert(!kGrad || kMode == kSchurInit, "the gradient comes with the init pass");
   constexpr int S0p = (S0 + 1) & ~1;
-  constexpr int kRec = kGrad ? 2 * S0p : S0p;  // doubles per contribution record
+  constexpr int kRec = S0p;                 // doubles per contribution record
   constexpr int kF = 2 * S0;                // doubles per F cell
-  constexpr int kImg = kWave * (kF + 6);    // F cells, then E cells, of up to a wave of blocks
-  static_assert(kF % 2 == 0 && kWave * kRec <= kImg, "16-byte pieces; contributions fit");
+  // F cells (not for init), then E cells, of up to a wave of blocks: init's
+  // smaller image lets more waves stay resident.
+  constexpr int kFImg = kMode == kSchurInit ? 0 : kWave * kF;
+  constexpr int kImg = kFImg + kWave * 6;
+  static_assert(kF % 2 == 0 && (kMode == kSchurInit || kWave * kRec <= kImg),
+                "16-byte pieces; contributions fit");
   __shared__ double img_all[kWPB][kImg];
   const int lane = threadIdx.x & (kWave - 1), wave = kWPB == 1 ? 0 : threadIdx.x / kWave;
   const int64_t c = (int64_t)blockIdx.x * kWPB + wave;
@@ -222,16 +230,18 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
     const double* segF = a.jac + a.f_base + (int64_t)kF * i0;
     const double* segE = a.jac + a.e_base + 6LL * i0;
     const int pf = (kF / 2) * nb, pe = 3 * nb;  // 16-byte pieces
+    if constexpr (kMode != kSchurInit) {
 #pragma unroll
-    for (int k = 0; k < kF / 2; ++k) {
-      const int p = k * kWave + lane;
-      if (p < pf) __builtin_amdgcn_global_load_lds(segF + 2 * p, im + 2 * kWave * k, 16, 0, 0);
+      for (int k = 0; k < kF / 2; ++k) {
+        const int p = k * kWave + lane;
+        if (p < pf) __builtin_amdgcn_global_load_lds(segF + 2 * p, im + 2 * kWave * k, 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int p = k * kWave + lane;
       if (p < pe)
-        __builtin_amdgcn_global_load_lds(segE + 2 * p, im + kWave * kF + 2 * kWave * k, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(segE + 2 * p, im + kFImg + 2 * kWave * k, 16, 0, 0);
     }
   }
   const long long idw = reinterpret_cast<const long long*>(a.ids)[i];
@@ -251,15 +261,17 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
   double F[kF], E[6];
+  if constexpr (kMode != kSchurInit) {
 #pragma unroll
-  for (int k = 0; k < kF / 2; ++k) {
-    const double2 v = reinterpret_cast<const double2*>(im + kF * lane)[k];
-    F[2 * k] = v.x;
-    F[2 * k + 1] = v.y;
+    for (int k = 0; k < kF / 2; ++k) {
+      const double2 v = reinterpret_cast<const double2*>(im + kF * lane)[k];
+      F[2 * k] = v.x;
+      F[2 * k + 1] = v.y;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const double2 v = reinterpret_cast<const double2*>(im + kWave * kF + 6 * lane)[k];
+    const double2 v = reinterpret_cast<const double2*>(im + kFImg + 6 * lane)[k];
     E[2 * k] = v.x;
     E[2 * k + 1] = v.y;
   }
@@ -333,6 +345,8 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
       yp[1] = w[1];
       yp[2] = w[2];
     }
+  } else if constexpr (kMode == kSchurInit) {
+    if (active) SchurStoreU<kGrad>(a, i, E, z, w);
   } else {
     // F_b^T u_b, staged over the consumed image, out as contiguous pieces.
     const double u0 = z[0] - (E[0] * w[0] + E[1] * w[1] + E[2] * w[2]);
@@ -344,14 +358,6 @@ __global__ __launch_bounds__(kWPB * kWave) void SchurChunkKernel(const SchurArgs
       const double c0 = F[2 * k] * u0 + F[S0 + 2 * k] * u1;
       const double c1 = 2 * k + 1 < S0 ? F[2 * k + 1] * u0 + F[S0 + 2 * k + 1] * u1 : 0.0;
       reinterpret_cast<double2*>(im + kRec * lane)[k] = make_double2(c0, c1);
-    }
-    if constexpr (kGrad) {  // -F_b^T b_b after them
-#pragma unroll
-      for (int k = 0; k < S0p / 2; ++k) {
-        const double c0 = -(F[2 * k] * z[0] + F[S0 + 2 * k] * z[1]);
-        const double c1 = 2 * k + 1 < S0 ? -(F[2 * k + 1] * z[0] + F[S0 + 2 * k + 1] * z[1]) : 0.0;
-        reinterpret_cast<double2*>(im + kRec * lane)[S0p / 2 + k] = make_double2(c0, c1);
-      }
     }
     __builtin_amdgcn_wave_barrier();
     typedef double v2d __attribute__((ext_vector_type(2)));
@@ -428,12 +434,22 @@ __global__ __launch_bounds__(kBlockThreads) void SchurBigKernel(const SchurArgs 
       a.y[ecol + 1] = w[1];
       a.y[ecol + 2] = w[2];
     }
+  } else if constexpr (kMode == kSchurInit) {
+    for (int64_t i = i0 + lane; i < i1; i += kWave) {
+      const double* ep = a.jac + a.e_base + 6 * i;
+      double E[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) E[k] = ep[k];
+      const double2 v = *reinterpret_cast<const double2*>(a.b + a.b_base + 2 * i);
+      const double z[2] = {v.x, v.y};
+      SchurStoreU<kGrad>(a, i, E, z, w);
+    }
   } else {
     for (int64_t i = i0 + lane; i < i1; i += kWave) {
       const int id0 = (int)reinterpret_cast<const long long*>(a.ids)[i];
       double F[2 * S0], E[6], z[2];
       SchurLoadBlock<S0, kMode>(a, i, id0, F, E, z);
-      SchurContrib<S0, kGrad>(a, i, F, E, z, w);
+      SchurContrib<S0>(a, i, F, E, z, w);
     }
   }
 }
@@ -459,30 +475,44 @@ __global__ __launch_bounds__(kBlockThreads) void AxpyKernel(const double* x, dou
   if (k < n) y[k] += x[k];
 }
 
-// Block diagonal preconditioners over the f blocks, per block list chunk
-// (the camera plan of the gradient: chunks of at most kGradChunk rows of one
-// f block), one wave per chunk, each lane summing the packed upper
-// triangle of F_b^T Q_b F_b over its rows:
-//   JACOBI        Q_b = I: (F^T F + D_f^2)^-1, ImplicitSchurComplement's
+// The init's camera-order pass, one wave per block list chunk (the camera
+// plan of the gradient: chunks of at most kGradChunk rows of one f block,
+// taken pass-major when `order` is given), each lane summing over its rows
+//     F_b^T u_b                       rhs = F^T (b - E M E^T b)
+//     F_b^T b_b      (kGrad)          the gradient's f rows, -F^T b
+//     F_b^T Q_b F_b  (kDiag, packed upper triangle) with
+//   kDiag 1, JACOBI        Q_b = I: (F^T F + D_f^2)^-1, ImplicitSchurComplement's
 //                 block_diagonal_FtF_inverse (implicit_schur_complement.cc:
 //                 71-95, iterative_schur_complement_solver.cc:186-189);
-//   SCHUR_JACOBI  Q_b = I - E_b M_p E_b^T: the f-block diagonal of S
+//   kDiag 2, SCHUR_JACOBI  Q_b = I - E_b M_p E_b^T: the f-block diagonal of S
 //                 (schur_jacobi_preconditioner.cc:89-98; exact when no e
-//                 block sees one f block twice, which the host checks).
+//                 block sees one f block twice, which the host checks),
+// then a fixed butterfly; the chunk's sums go to partial[cid][kPart].
+// Each F cell is read once per init, here; the point-order pass read only
+// the E cells.
 template <int S0>
 constexpr int SymCount() { return S0 * (S0 + 1) / 2; }
 
-template <int S0, bool kSchur>
-__global__ __launch_bounds__(kBlockThreads) void SchurBlockDiagKernel(const SchurArgs a,
-                                                                      const int32_t* perm,
-                                                                      const GradChunks ch) {
-  constexpr int T = SymCount<S0>();
+template <int S0, int kDiag, bool kGrad>
+constexpr int SchurPartCount() { return (kDiag ? SymCount<S0>() : 0) + S0 + (kGrad ? S0 : 0); }
+
+template <int S0, int kDiag, bool kGrad>
+__global__ __launch_bounds__(kBlockThreads) void SchurCameraPassKernel(const SchurArgs a,
+                                                                       const int32_t* perm,
+                                                                       const GradChunks ch,
+                                                                       const int32_t* order) {
+  constexpr int T = kDiag ? SymCount<S0>() : 1;
+  constexpr int kPart = SchurPartCount<S0, kDiag, kGrad>();
+  constexpr int kU = kGrad ? 4 : 2;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int64_t cid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  if (cid >= ch.nchunks) return;
-  double acc[T];
+  const int64_t slot = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (slot >= ch.nchunks) return;
+  const int64_t cid = order ? (int64_t)order[slot] : slot;
+  double acc[T], ru[S0], rb[S0];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = 0.0;
+#pragma unroll
+  for (int k = 0; k < S0; ++k) ru[k] = rb[k] = 0.0;
   const int64_t q1 = ch.begin[cid + 1];
   for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
     const int64_t i = perm[q];
@@ -494,125 +524,181 @@ __global__ __launch_bounds__(kBlockThreads) void SchurBlockDiagKernel(const Schu
       F[2 * k] = v.x;
       F[2 * k + 1] = v.y;
     }
-    double q00 = 1.0, q01 = 0.0, q11 = 1.0;
-    if constexpr (kSchur) {
-      const int id1 = (int)(reinterpret_cast<const long long*>(a.ids)[i] >> 32);
-      const double* m = a.ete_inv + 2 * (a.e_col_base + 3LL * id1);
-      double M[6], E[6];
+    const double2* up = reinterpret_cast<const double2*>(a.ub + kU * i);
+    const double2 u = up[0];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) M[k] = m[k];
-      const double* ep = a.jac + a.e_base + 6 * i;
+    for (int k = 0; k < S0; ++k) ru[k] += F[k] * u.x + F[S0 + k] * u.y;
+    if constexpr (kGrad) {
+      const double2 bb = up[1];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) E[k] = ep[k];
-      double me0[3], me1[3];
-      SymMul3(M, E, me0);
-      SymMul3(M, E + 3, me1);
-      q00 = 1.0 - (E[0] * me0[0] + E[1] * me0[1] + E[2] * me0[2]);
-      q01 = -(E[0] * me1[0] + E[1] * me1[1] + E[2] * me1[2]);
-      q11 = 1.0 - (E[3] * me1[0] + E[4] * me1[1] + E[5] * me1[2]);
+      for (int k = 0; k < S0; ++k) rb[k] += F[k] * bb.x + F[S0 + k] * bb.y;
     }
-    // F^T Q F, upper triangle row by row.
-    double g0[S0], g1[S0];  // Q F columns: rows 0 and 1
+    if constexpr (kDiag != 0) {
+      double q00 = 1.0, q01 = 0.0, q11 = 1.0;
+      if constexpr (kDiag == 2) {
+        const int id1 = (int)(reinterpret_cast<const long long*>(a.ids)[i] >> 32);
+        const double* m = a.ete_inv + 2 * (a.e_col_base + 3LL * id1);
+        double M[6], E[6];
 #pragma unroll
-    for (int k = 0; k < S0; ++k) {
-      g0[k] = q00 * F[k] + q01 * F[S0 + k];
-      g1[k] = q01 * F[k] + q11 * F[S0 + k];
+        for (int k = 0; k < 6; ++k) M[k] = m[k];
+        const double* ep = a.jac + a.e_base + 6 * i;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) E[k] = ep[k];
+        double me0[3], me1[3];
+        SymMul3(M, E, me0);
+        SymMul3(M, E + 3, me1);
+        q00 = 1.0 - (E[0] * me0[0] + E[1] * me0[1] + E[2] * me0[2]);
+        q01 = -(E[0] * me1[0] + E[1] * me1[1] + E[2] * me1[2]);
+        q11 = 1.0 - (E[3] * me1[0] + E[4] * me1[1] + E[5] * me1[2]);
+      }
+      // F^T Q F, upper triangle row by row.
+      double g0[S0], g1[S0];  // Q F columns: rows 0 and 1
+#pragma unroll
+      for (int k = 0; k < S0; ++k) {
+        g0[k] = q00 * F[k] + q01 * F[S0 + k];
+        g1[k] = q01 * F[k] + q11 * F[S0 + k];
+      }
+      int t = 0;
+#pragma unroll
+      for (int r = 0; r < S0; ++r)
+#pragma unroll
+        for (int cc = r; cc < S0; ++cc) acc[t++] += F[r] * g0[cc] + F[S0 + r] * g1[cc];
     }
-    int t = 0;
-#pragma unroll
-    for (int r = 0; r < S0; ++r)
-#pragma unroll
-      for (int cc = r; cc < S0; ++cc) acc[t++] += F[r] * g0[cc] + F[S0 + r] * g1[cc];
   }
 #pragma unroll
-  for (int t = 0; t < T; ++t)
+  for (int off = 32; off > 0; off >>= 1) {
+    if constexpr (kDiag != 0) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc[t] += __shfl_xor(acc[t], off, kWave);
+      for (int t = 0; t < T; ++t) acc[t] += __shfl_xor(acc[t], off, kWave);
+    }
+#pragma unroll
+    for (int k = 0; k < S0; ++k) ru[k] += __shfl_xor(ru[k], off, kWave);
+    if constexpr (kGrad) {
+#pragma unroll
+      for (int k = 0; k < S0; ++k) rb[k] += __shfl_xor(rb[k], off, kWave);
+    }
+  }
   if (lane == 0) {
+    double* out = ch.partial + cid * kPart;
+    if constexpr (kDiag != 0) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) ch.partial[cid * T + t] = acc[t];
+      for (int t = 0; t < T; ++t) out[t] = acc[t];
+      out += T;
+    }
+#pragma unroll
+    for (int k = 0; k < S0; ++k) out[k] = ru[k];
+    if constexpr (kGrad) {
+#pragma unroll
+      for (int k = 0; k < S0; ++k) out[S0 + k] = rb[k];
+    }
   }
 }
 
-// Per f block: its chunk partials summed in order, D^2 on the diagonal, the
-// inverse by the Cholesky factor (llt().solve(Identity), as the
-// reference's BlockRandomAccessDiagonalMatrix::Invert and AddDiagonalAndInvert)
-// stored as a full S0 x S0 matrix.
-template <int S0>
-__global__ __launch_bounds__(64) void SchurBlockInvertKernel(const GradChunks ch, int64_t count,
-                                                             const double* D, int64_t d_off,
-                                                             double* P, int* status) {
-  constexpr int T = SymCount<S0>();
+// Per f block p (thread p): its chunk partials summed in order; rhs rows
+// (rhs_p, S0 of them, assigned) and, kGrad, the gradient rows (grad_p,
+// -F^T b); kDiag: D^2 on the diagonal and the inverse by the Cholesky
+// factor (llt().solve(Identity), as the reference's
+// BlockRandomAccessDiagonalMatrix::Invert and AddDiagonalAndInvert) stored
+// as a full S0 x S0 matrix.
+template <int S0, int kDiag, bool kGrad>
+__global__ __launch_bounds__(64) void SchurCameraFinishKernel(const GradChunks ch, int64_t count,
+                                                              const double* D, int64_t d_off,
+                                                              double* P, int* status, double* rhs,
+                                                              double* grad) {
+  constexpr int T = kDiag ? SymCount<S0>() : 0;
+  constexpr int kPart = SchurPartCount<S0, kDiag, kGrad>();
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= count) return;
-  double L[S0][S0];
   {
-    double acc[T];
+    double ru[S0], rb[S0];
 #pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = 0.0;
-    for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q)
+    for (int k = 0; k < S0; ++k) ru[k] = rb[k] = 0.0;
+    for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q) {
+      const double* part = ch.partial + q * kPart + T;
 #pragma unroll
-      for (int t = 0; t < T; ++t) acc[t] += ch.partial[q * T + t];
-    int t = 0;
+      for (int k = 0; k < S0; ++k) ru[k] += part[k];
+      if constexpr (kGrad) {
 #pragma unroll
-    for (int r = 0; r < S0; ++r)
-#pragma unroll
-      for (int cc = r; cc < S0; ++cc) L[cc][r] = acc[t++];  // lower triangle of A
-  }
-  if (D) {
-#pragma unroll
-    for (int r = 0; r < S0; ++r) {
-      const double d = D[d_off + (int64_t)S0 * p + r];
-      L[r][r] += d * d;
-    }
-  }
-  // In-place Cholesky: A = L L^T.  A pivot that is not positive (a camera
-  // with no observation and D = NULL) raises the status word and leaves
-  // the block's inverse zero.
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < S0; ++j) {
-    double djj = L[j][j];
-#pragma unroll
-    for (int k = 0; k < j; ++k) djj -= L[j][k] * L[j][k];
-    ok = ok && PivotOk(djj);
-    const double ljj = sqrt(djj);
-    const double inv = 1.0 / ljj;
-    L[j][j] = ljj;
-#pragma unroll
-    for (int r = j + 1; r < S0; ++r) {
-      double v = L[r][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) v -= L[r][k] * L[j][k];
-      L[r][j] = v * inv;
-    }
-  }
-  double* out = P + (int64_t)S0 * S0 * p;
-  if (!ok) {
-    *status = 1;
-    for (int k = 0; k < S0 * S0; ++k) out[k] = 0.0;
-    return;
-  }
-  // Columns of the inverse: L y = e_c, then L^T x = y.
-#pragma unroll
-  for (int cc = 0; cc < S0; ++cc) {
-    double y[S0];
-#pragma unroll
-    for (int r = 0; r < S0; ++r) {
-      double v = r == cc ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < r; ++k) v -= L[r][k] * y[k];
-      y[r] = v / L[r][r];
+        for (int k = 0; k < S0; ++k) rb[k] += part[S0 + k];
+      }
     }
 #pragma unroll
-    for (int r = S0 - 1; r >= 0; --r) {
-      double v = y[r];
+    for (int k = 0; k < S0; ++k) rhs[(int64_t)S0 * p + k] = ru[k];
+    if constexpr (kGrad) {
 #pragma unroll
-      for (int k = r + 1; k < S0; ++k) v -= L[k][r] * y[k];
-      y[r] = v / L[r][r];
+      for (int k = 0; k < S0; ++k) grad[(int64_t)S0 * p + k] = -rb[k];
     }
+  }
+  if constexpr (kDiag != 0) {
+    double L[S0][S0];
+    {
+      double acc[T];
 #pragma unroll
-    for (int r = 0; r < S0; ++r) out[r * S0 + cc] = y[r];
+      for (int t = 0; t < T; ++t) acc[t] = 0.0;
+      for (int64_t q = ch.chunk_off[p]; q < ch.chunk_off[p + 1]; ++q)
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc[t] += ch.partial[q * kPart + t];
+      int t = 0;
+#pragma unroll
+      for (int r = 0; r < S0; ++r)
+#pragma unroll
+        for (int cc = r; cc < S0; ++cc) L[cc][r] = acc[t++];  // lower triangle of A
+    }
+    if (D) {
+#pragma unroll
+      for (int r = 0; r < S0; ++r) {
+        const double d = D[d_off + (int64_t)S0 * p + r];
+        L[r][r] += d * d;
+      }
+    }
+    // In-place Cholesky: A = L L^T.  A pivot that is not positive (a camera
+    // with no observation and D = NULL) raises the status word and leaves
+    // the block's inverse zero.
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < S0; ++j) {
+      double djj = L[j][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) djj -= L[j][k] * L[j][k];
+      ok = ok && PivotOk(djj);
+      const double ljj = sqrt(djj);
+      const double inv = 1.0 / ljj;
+      L[j][j] = ljj;
+#pragma unroll
+      for (int r = j + 1; r < S0; ++r) {
+        double v = L[r][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) v -= L[r][k] * L[j][k];
+        L[r][j] = v * inv;
+      }
+    }
+    double* out = P + (int64_t)S0 * S0 * p;
+    if (!ok) {
+      *status = 1;
+      for (int k = 0; k < S0 * S0; ++k) out[k] = 0.0;
+      return;
+    }
+    // Columns of the inverse: L y = e_c, then L^T x = y.
+#pragma unroll
+    for (int cc = 0; cc < S0; ++cc) {
+      double y[S0];
+#pragma unroll
+      for (int r = 0; r < S0; ++r) {
+        double v = r == cc ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < r; ++k) v -= L[r][k] * y[k];
+        y[r] = v / L[r][r];
+      }
+#pragma unroll
+      for (int r = S0 - 1; r >= 0; --r) {
+        double v = y[r];
+#pragma unroll
+        for (int k = r + 1; k < S0; ++k) v -= L[k][r] * y[k];
+        y[r] = v / L[r][r];
+      }
+#pragma unroll
+      for (int r = 0; r < S0; ++r) out[r * S0 + cc] = y[r];
+    }
   }
 }
 

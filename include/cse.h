@@ -436,11 +436,12 @@ int cse_schur_init(cse_evaluator* ev, const double* d_jacobian_values, const dou
  * d_gradient (num_effective_parameters entries, assigned), taking r = -b --
  * the trust-region step's b (TrustRegionMinimizer::EvaluateGradientAndJacobian
  * evaluates g = J^T r beside J, trust_region_minimizer.cc:242-255) -- in the
- * same pass over J: the e rows from the E^T b sums the init forms anyway,
- * the f rows from a second half of each block's contribution record.  Then
- * the evaluation before it needs no gradient (no CameraGradientKernel).
- * Deterministic; equals the evaluation's gradient (gradient_mode 0) to
- * rounding (a different summation order). */
+ * same passes over J: the e rows from the E^T b sums the init forms anyway,
+ * the f rows -F^T b in the camera-order pass that forms F^T u and the
+ * preconditioner, from b_b stored beside u_b.  Then the evaluation before it
+ * needs no gradient (no CameraGradientKernel).  Deterministic; equals the
+ * evaluation's gradient (gradient_mode 0) to rounding (a different
+ * summation order). */
 int cse_schur_init_gradient(cse_evaluator* ev, const double* d_jacobian_values, const double* d_D,
                             const double* d_b, double* d_rhs, int preconditioner,
                             double* d_gradient);
