@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""A/B timing of the hot kernel's tuning variants (tuning build only).
+"""A/B timing of builds of the library in interleaved processes.
 
-Loads lib/libcse_tuning.so (make -C ceres-solver-cuda_amd tuning), builds one
-problem-13682-shaped Program, and times the residual+Jacobian evaluation for
-each $CSE_TUNE_VARIANT in interleaved rounds (so box drift hits all variants
-alike).  Every variant's residuals, Jacobian and cost are checked bit-equal
-to variant 0's (the variants change how the outputs are written, not what).
+Loads lib/libcse.so or --lib PATH (e.g. the previous commit's build), builds
+one problem-13682-shaped Program and times the residual+Jacobian evaluation
+in rounds.  Rounds 2-5 also selected tuning variants of one build through
+$CSE_TUNE_VARIANT (the tuning build, removed in round 6: the product reads no
+environment variable, so --variants 0 is the only meaningful value now).
+Every variant's residuals, Jacobian and cost are checked bit-equal to
+variant 0's.
 
-  python tools/ab_bench.py --variants 0,1,2,3,5 --rounds 3 --steps 20
+  python tools/ab_bench.py --lib other/libcse.so --variants 0 --rounds 3 --steps 20
 """
 import argparse
 import hashlib
@@ -23,8 +25,8 @@ import numpy as np  # noqa: E402
 
 from ceres_amd import _cse  # noqa: E402
 
-_LIB = os.path.join(REPO, "ceres-solver-cuda_amd", "lib", "libcse_tuning.so")
-if "--lib" in sys.argv:  # another tuning build of the same ABI (e.g. the previous commit's)
+_LIB = os.path.join(REPO, "ceres-solver-cuda_amd", "lib", "libcse.so")
+if "--lib" in sys.argv:  # another build of the same ABI (e.g. the previous commit's)
     _LIB = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 _cse.use_library(_LIB)
 
@@ -34,13 +36,13 @@ from ceres_amd import bal  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--variants", default="0")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--config", default="problem-13682-4456117")
     ap.add_argument("--loss", default="huber")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--lib", default=None, help="tuning library to load (default lib/libcse_tuning.so)")
+    ap.add_argument("--lib", default=None, help="library to load (default lib/libcse.so)")
     ap.add_argument("--mode", default="jacobian", choices=["jacobian", "gradient", "residual", "cost"])
     ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
     ap.add_argument("--held-cameras", type=int, default=0,
