@@ -477,17 +477,29 @@ __global__ __launch_bounds__(kBlockThreads) void AxpyKernel(const double* x, dou
 
 // The init's camera-order pass, one wave per block list chunk (the camera
 // plan of the gradient: chunks of at most kGradChunk rows of one f block,
-// taken pass-major when `order` is given), each lane summing over its rows
-//     F_b^T u_b                       rhs = F^T (b - E M E^T b)
-//     F_b^T b_b      (kGrad)          the gradient's f rows, -F^T b
-//     F_b^T Q_b F_b  (kDiag, packed upper triangle) with
+// taken pass-major when `order` is given).  Over the chunk's rows k (two per
+// residual block) it forms, for its f block,
+//     F^T u          rhs = F^T (b - E M E^T b)
+//     F^T b          (kGrad) the gradient's f rows, -F^T b
+//     F^T Q F        (kDiag) the preconditioner's block, with
 //   kDiag 1, JACOBI        Q_b = I: (F^T F + D_f^2)^-1, ImplicitSchurComplement's
 //                 block_diagonal_FtF_inverse (implicit_schur_complement.cc:
 //                 71-95, iterative_schur_complement_solver.cc:186-189);
 //   kDiag 2, SCHUR_JACOBI  Q_b = I - E_b M_p E_b^T: the f-block diagonal of S
 //                 (schur_jacobi_preconditioner.cc:89-98; exact when no e
 //                 block sees one f block twice, which the host checks),
-// then a fixed butterfly; the chunk's sums go to partial[cid][kPart].
+// as ONE matrix product on the matrix cores: C (16 x 16) += A^T B over the
+// chunk's rows, A = [F rows] (9 of 16 columns), B = [rows of Q F | u | b]
+// (columns 0-8, 9, 10): C[0:9, 0:9] = F^T Q F, C[0:9, 9] = F^T u,
+// C[0:9, 10] = F^T b.  Per slab of 32 blocks, two lanes gather each block
+// (half the F cell each; the second also u_b and b_b; for Q both read E_b
+// and M_p and each writes one row of Q F) into the wave's LDS slab; 16
+// v_mfma_f64_16x16x4_f64 then take the slab's 64 rows, four at a time
+// (lane l supplies row 4s + l/16, column l % 16 of A and of B).  The
+// accumulator is 4 doubles per lane instead of the 63 sums a lane-per-block
+// form keeps (248 VGPRs, 2 waves per SIMD): 42 VGPRs and 7 waves per SIMD
+// here (4 for SCHUR_JACOBI).  Fixed order: bit-identical run to run.  The chunk's
+// sums go to partial[cid][kPart] (upper triangle, then F^T u, then F^T b).
 // Each F cell is read once per init, here; the point-order pass read only
 // the E cells.
 template <int S0>
@@ -501,41 +513,68 @@ __global__ __launch_bounds__(kBlockThreads) void SchurCameraPassKernel(const Sch
                                                                        const int32_t* perm,
                                                                        const GradChunks ch,
                                                                        const int32_t* order) {
-  constexpr int T = kDiag ? SymCount<S0>() : 1;
+  static_assert(S0 + 2 <= 16, "A^T B in one 16 x 16 f64 tile");
+  constexpr int T = kDiag ? SymCount<S0>() : 0;
   constexpr int kPart = SchurPartCount<S0, kDiag, kGrad>();
   constexpr int kU = kGrad ? 4 : 2;
+  constexpr int kG = kDiag == 2 ? S0 : 0;  // Q F columns after F
+  constexpr int kW = S0 + kG + 2;          // doubles per LDS row: F | Q F | u | b
+  constexpr int kSlab = kWave / 2;         // blocks per slab: two lanes per block
+  constexpr int kRows = 2 * kSlab;         // rows per slab
+  typedef double v4d __attribute__((ext_vector_type(4)));
+  __shared__ double slab_all[kWavesPerBlock][kRows * kW];
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int64_t slot = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (slot >= ch.nchunks) return;
+  double* slab = slab_all[wave];
   const int64_t cid = order ? (int64_t)order[slot] : slot;
-  double acc[T], ru[S0], rb[S0];
+  const int64_t q0 = ch.begin[cid], q1 = ch.begin[cid + 1];
+  const int col = lane & 15, rsub = lane >> 4;
+  const int bl = lane & (kSlab - 1), h = lane / kSlab;  // block of the slab, half of its cell
+  constexpr int kP0 = (S0 + 1) / 2;                      // 16-byte pieces of half 0
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t qs = q0; qs < q1; qs += kSlab) {
+    const int nb = (int)(q1 - qs < kSlab ? q1 - qs : kSlab);
+    int64_t i = 0;
+    if (bl < nb) {
+      i = perm[qs + bl];
+      // half 0: F doubles [0, 2 kP0); half 1: [2 kP0, 2 S0), u_b (and b_b).
+      const double2* fp = reinterpret_cast<const double2*>(a.jac + a.f_base + 2 * S0 * i);
+      double* r0 = slab + (2 * bl) * kW;
+      if (h == 0) {
 #pragma unroll
-  for (int t = 0; t < T; ++t) acc[t] = 0.0;
+        for (int k = 0; k < kP0; ++k) {
+          const double2 v = fp[k];
+          const int d = 2 * k;
+          r0[(d / S0) * kW + d % S0] = v.x;
+          r0[((d + 1) / S0) * kW + (d + 1) % S0] = v.y;
+        }
+      } else {
 #pragma unroll
-  for (int k = 0; k < S0; ++k) ru[k] = rb[k] = 0.0;
-  const int64_t q1 = ch.begin[cid + 1];
-  for (int64_t q = ch.begin[cid] + lane; q < q1; q += kWave) {
-    const int64_t i = perm[q];
-    double F[2 * S0];
-    const double2* fp = reinterpret_cast<const double2*>(a.jac + a.f_base + 2 * S0 * i);
-#pragma unroll
-    for (int k = 0; k < S0; ++k) {
-      const double2 v = fp[k];
-      F[2 * k] = v.x;
-      F[2 * k + 1] = v.y;
+        for (int k = kP0; k < S0; ++k) {
+          const double2 v = fp[k];
+          const int d = 2 * k;
+          r0[(d / S0) * kW + d % S0] = v.x;
+          r0[((d + 1) / S0) * kW + (d + 1) % S0] = v.y;
+        }
+        const double2* up = reinterpret_cast<const double2*>(a.ub + kU * i);
+        const double2 u = up[0];
+        r0[S0 + kG] = u.x;
+        r0[kW + S0 + kG] = u.y;
+        if constexpr (kGrad) {
+          const double2 bb = up[1];
+          r0[S0 + kG + 1] = bb.x;
+          r0[kW + S0 + kG + 1] = bb.y;
+        } else {
+          r0[S0 + kG + 1] = 0.0;
+          r0[kW + S0 + kG + 1] = 0.0;
+        }
+      }
     }
-    const double2* up = reinterpret_cast<const double2*>(a.ub + kU * i);
-    const double2 u = up[0];
-#pragma unroll
-    for (int k = 0; k < S0; ++k) ru[k] += F[k] * u.x + F[S0 + k] * u.y;
-    if constexpr (kGrad) {
-      const double2 bb = up[1];
-#pragma unroll
-      for (int k = 0; k < S0; ++k) rb[k] += F[k] * bb.x + F[S0 + k] * bb.y;
-    }
-    if constexpr (kDiag != 0) {
-      double q00 = 1.0, q01 = 0.0, q11 = 1.0;
-      if constexpr (kDiag == 2) {
+    if constexpr (kDiag == 2) {
+      // Q F rows: half h writes row h of its block, from the F rows above.
+      double q0v = 0.0, q1v = 0.0;
+      if (bl < nb) {
         const int id1 = (int)(reinterpret_cast<const long long*>(a.ids)[i] >> 32);
         const double* m = a.ete_inv + 2 * (a.e_col_base + 3LL * id1);
         double M[6], E[6];
@@ -547,49 +586,52 @@ __global__ __launch_bounds__(kBlockThreads) void SchurCameraPassKernel(const Sch
         double me0[3], me1[3];
         SymMul3(M, E, me0);
         SymMul3(M, E + 3, me1);
-        q00 = 1.0 - (E[0] * me0[0] + E[1] * me0[1] + E[2] * me0[2]);
-        q01 = -(E[0] * me1[0] + E[1] * me1[1] + E[2] * me1[2]);
-        q11 = 1.0 - (E[3] * me1[0] + E[4] * me1[1] + E[5] * me1[2]);
+        const double q00 = 1.0 - (E[0] * me0[0] + E[1] * me0[1] + E[2] * me0[2]);
+        const double q01 = -(E[0] * me1[0] + E[1] * me1[1] + E[2] * me1[2]);
+        const double q11 = 1.0 - (E[3] * me1[0] + E[4] * me1[1] + E[5] * me1[2]);
+        q0v = h == 0 ? q00 : q01;
+        q1v = h == 0 ? q01 : q11;
       }
-      // F^T Q F, upper triangle row by row.
-      double g0[S0], g1[S0];  // Q F columns: rows 0 and 1
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      if (bl < nb) {
+        const double* f0 = slab + (2 * bl) * kW;
+        double* g = slab + (2 * bl + h) * kW + S0;
 #pragma unroll
-      for (int k = 0; k < S0; ++k) {
-        g0[k] = q00 * F[k] + q01 * F[S0 + k];
-        g1[k] = q01 * F[k] + q11 * F[S0 + k];
+        for (int k = 0; k < S0; ++k) g[k] = q0v * f0[k] + q1v * f0[kW + k];
       }
-      int t = 0;
-#pragma unroll
-      for (int r = 0; r < S0; ++r)
-#pragma unroll
-        for (int cc = r; cc < S0; ++cc) acc[t++] += F[r] * g0[cc] + F[S0 + r] * g1[cc];
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // A[m][k] = row k, column m (F); B[k][n] = row k, column n of [Q F | u | b]
+    // (columns 0-8 of B are F's own for JACOBI; none for IDENTITY).
+    const int bcol = col < S0 ? (kDiag == 0 ? -1 : kDiag == 2 ? S0 + col : col)
+                              : col == S0 ? S0 + kG : (kGrad && col == S0 + 1) ? S0 + kG + 1 : -1;
+    const int rows = 2 * nb;
+#pragma unroll 4
+    for (int s = 0; s < kRows / 4; ++s) {
+      const int row = 4 * s + rsub;
+      if (4 * s >= rows) break;
+      const bool live = row < rows;
+      const double av = live && col < S0 ? slab[row * kW + col] : 0.0;
+      const double bv = live && bcol >= 0 ? slab[row * kW + bcol] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
   }
+  // C[m][n]: m = lane / 16 + 4 r, n = lane % 16.
+  double* out = ch.partial + cid * kPart;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
+  for (int r = 0; r < 4; ++r) {
+    const int m = rsub + 4 * r, n = col;
+    if (m >= S0) continue;
     if constexpr (kDiag != 0) {
-#pragma unroll
-      for (int t = 0; t < T; ++t) acc[t] += __shfl_xor(acc[t], off, kWave);
+      if (n < S0 && m <= n) out[m * S0 - m * (m - 1) / 2 + (n - m)] = acc[r];
     }
-#pragma unroll
-    for (int k = 0; k < S0; ++k) ru[k] += __shfl_xor(ru[k], off, kWave);
+    if (n == S0) out[T + m] = acc[r];
     if constexpr (kGrad) {
-#pragma unroll
-      for (int k = 0; k < S0; ++k) rb[k] += __shfl_xor(rb[k], off, kWave);
-    }
-  }
-  if (lane == 0) {
-    double* out = ch.partial + cid * kPart;
-    if constexpr (kDiag != 0) {
-#pragma unroll
-      for (int t = 0; t < T; ++t) out[t] = acc[t];
-      out += T;
-    }
-#pragma unroll
-    for (int k = 0; k < S0; ++k) out[k] = ru[k];
-    if constexpr (kGrad) {
-#pragma unroll
-      for (int k = 0; k < S0; ++k) out[S0 + k] = rb[k];
+      if (n == S0 + 1) out[T + S0 + m] = acc[r];
     }
   }
 }

@@ -193,9 +193,12 @@ def test_schur_init_reports_singular_blocks_without_D(gpu):
     ev.close()
 
 
-@pytest.mark.parametrize("which", ["bal", "runs", "quaternion", "large"])
-@pytest.mark.parametrize("with_D", [True, False])
-def test_schur_init_gradient_equals_evaluation_gradient(gpu, which, with_D):
+@pytest.mark.parametrize("which,with_D,precond",
+                         [(w, d, _cse.SCHUR_JACOBI) for w in ("bal", "runs", "quaternion", "large")
+                          for d in (True, False)] +
+                         [(w, True, p) for w in ("bal", "runs")
+                          for p in (_cse.SCHUR_IDENTITY, _cse.SCHUR_SCHUR_JACOBI)])
+def test_schur_init_gradient_equals_evaluation_gradient(gpu, which, with_D, precond):
     """cse_schur_init_gradient: the init also writes
     g = J^T r (r = -b) -- what TrustRegionMinimizer::EvaluateGradientAndJacobian
     (trust_region_minimizer.cc:242-255) gets from the evaluator beside J --
@@ -222,10 +225,10 @@ def test_schur_init_gradient_equals_evaluation_gradient(gpu, which, with_D):
     rhs0 = torch.empty(f_cols, dtype=torch.float64, device=dev)
     rhs1 = torch.full((f_cols,), np.nan, dtype=torch.float64, device=dev)
     dg = torch.full((n,), np.nan, dtype=torch.float64, device=dev)
-    ev.schur_init_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs0.data_ptr(), _cse.SCHUR_JACOBI)
+    ev.schur_init_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs0.data_ptr(), precond)
     rc0 = ev.wait()
     ev.schur_init_gradient_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs1.data_ptr(),
-                                  dg.data_ptr(), _cse.SCHUR_JACOBI)
+                                  dg.data_ptr(), precond)
     rc1 = ev.wait()
     # without D the runs problem has singular point blocks: both inits say so
     assert rc0 == rc1
@@ -240,9 +243,18 @@ def test_schur_init_gradient_equals_evaluation_gradient(gpu, which, with_D):
     # bit-identical (fixed-order sums)
     dg2 = torch.empty_like(dg)
     ev.schur_init_gradient_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs1.data_ptr(),
-                                  dg2.data_ptr(), _cse.SCHUR_JACOBI)
+                                  dg2.data_ptr(), precond)
     ev.wait()
     assert torch.equal(dg, dg2)
+    # the preconditioner built beside the gradient is the plain init's
+    x = torch.from_numpy(np.random.default_rng(4).normal(size=f_cols)).to(dev)
+    y0 = torch.zeros(f_cols, dtype=torch.float64, device=dev)
+    y1 = torch.zeros(f_cols, dtype=torch.float64, device=dev)
+    ev.schur_precondition_device(x.data_ptr(), y1.data_ptr())
+    ev.schur_init_device(dj.data_ptr(), D_ptr, db.data_ptr(), rhs0.data_ptr(), precond)
+    ev.schur_precondition_device(x.data_ptr(), y0.data_ptr())
+    ev.wait()
+    assert torch.equal(y0, y1)
     ev.close()
 
 
