@@ -218,3 +218,24 @@ def test_cgnr_operator_two_product_path(gpu):
     # functor types): not eligible for the fused pass.
     from test_parity_gpu import mini_ba
     assert cgnr_op_check(mini_ba(ca.BLOCK_SPARSE), seed=2) == 0
+
+
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+def test_left_multiply_by_residuals_is_the_gradient(gpu, fmt):
+    """A device CGNR step forms its right-hand side Jᵀ(−r) with
+    cse_jacobian_left_multiply; with it the evaluation before needs no
+    gradient either (as cse_schur_init_gradient for ITERATIVE_SCHUR):
+    Jᵀr from the operator equals gradient_mode 0's gradient to 1e-13."""
+    prog = bal.synthetic_program((24, 3000, 20000), loss=ca.Loss.huber(1.0), format=fmt, seed=12)
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
+    ok, cost, r, g, jv = ev.evaluate()
+    assert ok
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dj, dr = t(jv), t(r)
+    dg = torch.zeros(prog.num_effective_parameters, dtype=torch.float64, device=dev)
+    ev.left_multiply_device(dj.data_ptr(), dr.data_ptr(), dg.data_ptr())
+    torch.cuda.synchronize(dev)
+    got = dg.cpu().numpy()
+    assert np.abs(got - g).max() <= 1e-13 * np.abs(g).max()
+    ev.close()
