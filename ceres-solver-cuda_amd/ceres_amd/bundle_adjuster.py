@@ -123,12 +123,17 @@ def solve(args):
         timers.add(name, time.perf_counter() - s)
         return out
 
+    # ITERATIVE_SCHUR takes g = J^T r from its own init (cse_schur_init_gradient,
+    # every solve, before g is read); CGNR from the evaluation.
+    grad_from_init = args.linear_solver == "iterative_schur"
+
     def jacobian_eval(new_point=True):
         # After an accepted step x holds the candidate just evaluated:
         # new_evaluation_point = false, as HandleSuccessfulStep passes
         # (trust_region_minimizer.cc:822-826).
-        ev.evaluate_device(x.data_ptr(), cost.data_ptr(), r.data_ptr(), g.data_ptr(),
-                           jac.data_ptr(), new_evaluation_point=new_point)
+        ev.evaluate_device(x.data_ptr(), cost.data_ptr(), r.data_ptr(),
+                           None if grad_from_init else g.data_ptr(), jac.data_ptr(),
+                           new_evaluation_point=new_point)
         return ev.wait()
 
     def normal_op(v, sqrt_lam_d):
@@ -178,8 +183,8 @@ def solve(args):
         # reduced to S dx_f = rhs, PCG on S, then back substitution.
         torch.neg(r, out=neg_r)
         sqrt_lam_d = torch.sqrt(lam * D)
-        ev.schur_init_device(jac.data_ptr(), sqrt_lam_d.data_ptr(), neg_r.data_ptr(),
-                             rhs.data_ptr(), pre)
+        ev.schur_init_gradient_device(jac.data_ptr(), sqrt_lam_d.data_ptr(), neg_r.data_ptr(),
+                                      rhs.data_ptr(), g.data_ptr(), pre)
         xf = torch.zeros(f_cols, dtype=f64, device=dev)
         res = rhs.clone()
         z = torch.zeros_like(res)

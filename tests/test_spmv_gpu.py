@@ -164,6 +164,23 @@ def test_bundle_adjuster_driver_reduces_cost(gpu):
     assert all(r[-1] for r in rows)
 
 
+def test_bundle_adjuster_gradient_from_the_schur_init(gpu):
+    """The iterative_schur driver evaluates without the gradient and takes
+    g = Jᵀr from cse_schur_init_gradient; the cgnr driver takes it from the
+    evaluation.  At the same (deterministically perturbed) start both report
+    the same |g| and cost, and the Schur run's first step is accepted (its
+    model decrease -(g·dx + |J dx|²/2) uses that g)."""
+    from ceres_amd import bundle_adjuster
+    base = ["--synthetic", "problem-16-22106", "--robustify", "--point_sigma", "0.05",
+            "--num_iterations", "1"]
+    _, _, rows_s = bundle_adjuster.main(base + ["--linear_solver", "iterative_schur"])
+    _, _, rows_c = bundle_adjuster.main(base + ["--linear_solver", "cgnr"])
+    (_, c0s, _, gs, _, _, _, acc_s), (_, c0c, _, gc, _, _, _, _) = rows_s[0], rows_c[0]
+    assert c0s == c0c
+    assert abs(gs - gc) <= 1e-12 * gc and gs > 0
+    assert acc_s
+
+
 def cgnr_op_check(prog, seed, with_d=True):
     """cse_cgnr_multiply against J^T J x + D^2 x from the dense J; fused and
     two-product paths; deterministic."""
