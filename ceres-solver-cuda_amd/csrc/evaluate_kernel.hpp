@@ -1455,8 +1455,14 @@ __global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsKernel(const int
 // plus-Jacobian for manifold blocks, loss and Corrector, gradient atomics,
 // residuals and Jacobian rows scattered through the offset tables
 // (WriteJacobians, :260-294).
+// waves_per_eu(2, 2): at the default occupancy target the compiler keeps
+// the local Jacobian (NR x N doubles) in scratch (208 bytes a lane for
+// Snavely); with the register budget of two waves it lives in 126 VGPRs
+// (the hardware still fits four waves) and the general path of
+// problem-1778 BSM goes from 1.108 to 0.799 ms (profiles/round6/r6o).
 template <class K, int kLoss, bool kJac>
-__global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const GroupArgs a) {
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
+EvaluateTableKernel(const GroupArgs a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, NB = Tr::NB, N = Tr::N, D = Tr::D;
   static_assert(NB <= kMaxSlots, "too many parameter blocks");

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""The general (table) kernel against the affine fast path on one problem.
+
+Every functor shape outside the affine-validated set (user functors of other
+shapes, manifolds given as explicit plus-Jacobians, ...) runs
+EvaluateTableKernel.  This times both paths on the same BAL-shaped Program
+(cse_options.force_general_layout), device-resident residuals + Jacobian +
+cost, interleaved, and checks their outputs agree to 1e-13.
+
+  python tools/general_path_probe.py --config problem-1778-993923 --rounds 3
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ceres-solver-cuda_amd"))
+if "--lib" in sys.argv:  # another build of the same ABI (A/B)
+    from ceres_amd import _cse  # noqa: E402
+    _cse.use_library(os.path.abspath(sys.argv[sys.argv.index("--lib") + 1]))
+import ceres_amd as ca  # noqa: E402
+from ceres_amd import bal  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="problem-13682-4456117")
+    ap.add_argument("--format", default="block_sparse", choices=["block_sparse", "compressed_row"])
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="load this build of libcse.so")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    prog = bal.synthetic_program(args.config, loss=ca.Loss.huber(1.0), format=args.format)
+    f64 = torch.float64
+    state = torch.from_numpy(prog.state).to(dev)
+    out = {}
+    evs = {name: ca.Evaluator(prog, stream=stream.cuda_stream, force_general_layout=general)
+           for name, general in (("affine", False), ("table", True))}
+    bufs = {name: (torch.zeros(1, dtype=f64, device=dev),
+                   torch.empty(prog.num_residuals, dtype=f64, device=dev),
+                   torch.empty(prog.num_jacobian_values, dtype=f64, device=dev)) for name in evs}
+    times = {name: [] for name in evs}
+    for name, ev in evs.items():
+        info = ev.info()
+        out[name] = {"affine_groups": info.num_affine_groups}
+    for rnd in range(args.rounds):
+        for name, ev in evs.items():
+            c, r, j = bufs[name]
+            for _ in range(5):
+                ev.evaluate_device(state.data_ptr(), c.data_ptr(), r.data_ptr(), None, j.data_ptr())
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                ev.evaluate_device(state.data_ptr(), c.data_ptr(), r.data_ptr(), None, j.data_ptr())
+            torch.cuda.synchronize(dev)
+            assert ev.wait() == 0
+            times[name].append((time.perf_counter() - t0) / args.steps * 1e3)
+    a, t = bufs["affine"], bufs["table"]
+    rel = lambda x, y: float(torch.linalg.norm(x - y) / torch.linalg.norm(y))
+    for name in evs:
+        out[name]["ms_per_eval"] = sorted(times[name])[len(times[name]) // 2]
+        out[name]["rounds_ms"] = [round(x, 4) for x in times[name]]
+    out["table_over_affine"] = out["table"]["ms_per_eval"] / out["affine"]["ms_per_eval"]
+    out["rel_diff"] = {"cost": abs(float(a[0] - t[0])) / abs(float(t[0])),
+                       "residuals": rel(a[1], t[1]), "jacobian": rel(a[2], t[2])}
+    out["config"] = args.config
+    out["format"] = args.format
+    for ev in evs.values():
+        ev.close()
+    print(json.dumps(out), flush=True)
+    assert max(out["rel_diff"].values()) <= 1e-13
+
+
+if __name__ == "__main__":
+    main()
