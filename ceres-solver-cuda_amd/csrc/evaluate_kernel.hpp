@@ -1131,9 +1131,10 @@ __device__ __forceinline__ void AffineChunkBody(const GroupArgs& a) {
     }
     cb0 = a.gcontrib + (int64_t)(2 * kGQ) * i0 + 2 * lane + 512;
   }
-  // Residual pieces: the lane's own NR doubles (NR even).
+  // Residual pieces: the lane's own NR doubles (NR even; FastTail sends
+  // odd NR to the staged tail, the array only has to exist).
   constexpr int kQr = NR / 2;
-  cse_v4i qr[kQr];
+  cse_v4i qr[kQr > 0 ? kQr : 1];
 #pragma unroll
   for (int k = 0; k < kQr; ++k) qr[k] = AsV4i(r[2 * k], r[2 * k + 1]);
   double* rdst = a.residuals ? a.residuals + a.res_base + (int64_t)NR * (i0 + lane) : nullptr;

@@ -94,15 +94,19 @@ struct UserKind {
   }
 };
 
-// The functor shapes the affine kernels have been validated on against the
-// oracle (the library's own kinds: Snavely <2,9,3>, <2,7,3>, <2,10,3>, point
-// displacement <3,3>); a user kind of another shape runs the general kernel.
+// The shapes the affine kernels take for a user kind: the host's bound
+// (DetectAffine: one or two parameter blocks, at most three residuals),
+// slot sizes within one 128-byte row of the repacked slot-0 table
+// (PackedRowDoubles: at most 16 doubles) and 8 for slot 1, functors that
+// assign every output.  The library's own kinds cover <2, 9|7|10, 3> and
+// <3, 3> against the oracle; tests/test_user_functor_gpu.py checks the other
+// shapes of examples/user_functors.hip (<2, 6, 3> with six doubles of data,
+// <1, 6, 3>, <3, 6>) against the general kernel, which runs the same functor
+// one block per lane.  Other shapes run the general kernel.
 template <class K>
-constexpr bool kAffineValidatedShape =
-    !K::kMayLeaveOutputs &&
-    ((K::kNumResiduals == 2 && K::kNumBlocks == 2 && K::kSize1 == 3 &&
-      (K::kSize0 == 9 || K::kSize0 == 7 || K::kSize0 == 10)) ||
-     (K::kNumResiduals == 3 && K::kNumBlocks == 1 && K::kSize0 == 3));
+constexpr bool kAffineShape =
+    !K::kMayLeaveOutputs && K::kNumResiduals <= 3 && K::kNumBlocks <= 2 && K::kSize0 <= 16 &&
+    (K::kNumBlocks == 1 || K::kSize1 <= 8) && K::kDataSize <= 32;
 
 }  // namespace cse
 

@@ -17,8 +17,8 @@
 //
 // What the TU instantiates for (F, Loss, kR, Ns...): the library's general
 // kernel (EvaluateTableKernel, any shape up to 10 parameter blocks), and for
-// the shapes the affine kernels are validated on (cse::
-// kAffineValidatedShape: two blocks <2, 9|7|10, 3> or one block <3, 3>) the
+// the shapes the affine kernels take (cse::kAffineShape: one or two blocks,
+// at most three residuals, slot 0 at most 16 values, slot 1 at most 8) the
 // coalesced affine kernels with the LDS-DMA camera gather, their gradient
 // post-passes and J x / J^T x -- the same kernels, same settings, as a
 // built-in kind of that shape.  The Jacobian is always by Jet<double,
@@ -144,7 +144,7 @@ cse_functor_ops MakeOps(const char* name) {
   o.table[0] = &TableLaunch<K, L, false>;
   o.table[1] = &TableLaunch<K, L, true>;
   o.multiply = &MultiplyLaunch<K>;
-  if constexpr (cse::kAffineValidatedShape<K>) {
+  if constexpr (cse::kAffineShape<K>) {
     o.affine[0][0][0] = &AffineLaunch<K, L, false, false, false>;
     o.affine[0][0][1] = &AffineLaunch<K, L, false, false, true>;
     o.affine[0][1][0] = &AffineLaunch<K, L, false, true, false>;

@@ -156,6 +156,62 @@ struct OnlyFillsOneOutputFunctor {
   }
 };
 
+// Three functors of shapes outside the library's own kinds, the kind a
+// user brings: they run on the affine kernels through
+// ceres_amd/autodiff_cuda.h (tests/test_user_functor_gpu.py checks each
+// against the general kernel).
+//
+// Reprojection with a pose block (angle-axis, translation: 6) and a point
+// (3); the pinhole intrinsics travel in the functor (6 doubles of data).
+struct PoseReprojectionError {
+  PoseReprojectionError(double u, double v, double fx, double fy, double cx, double cy)
+      : u(u), v(v), fx(fx), fy(fy), cx(cx), cy(cy) {}
+  template <typename T>
+  HOST_DEVICE bool operator()(const T* const pose, const T* const point, T* residuals) const {
+    T p[3];
+    AngleAxisRotatePoint(pose, point, p);
+    p[0] += pose[3];
+    p[1] += pose[4];
+    p[2] += pose[5];
+    residuals[0] = fx * p[0] / p[2] + cx - u;
+    residuals[1] = fy * p[1] / p[2] + cy - v;
+    return true;
+  }
+  double u, v, fx, fy, cx, cy;
+};
+
+// Signed distance of a point (3), moved by a pose (6), to a plane n.x = d:
+// one residual, the plane in the functor (4 doubles).
+struct PointToPlaneError {
+  PointToPlaneError(double nx, double ny, double nz, double d) : nx(nx), ny(ny), nz(nz), d(d) {}
+  template <typename T>
+  HOST_DEVICE bool operator()(const T* const pose, const T* const point, T* residuals) const {
+    T q[3];
+    AngleAxisRotatePoint(pose, point, q);
+    residuals[0] = nx * (q[0] + pose[3]) + ny * (q[1] + pose[4]) + nz * (q[2] + pose[5]) - d;
+    return true;
+  }
+  double nx, ny, nz, d;
+};
+
+// Rigid alignment: a source point moved by one pose block (6) against its
+// target, three residuals; both points in the functor (6 doubles).
+struct RigidAlignmentError {
+  RigidAlignmentError(const double* src, const double* dst)
+      : sx(src[0]), sy(src[1]), sz(src[2]), tx(dst[0]), ty(dst[1]), tz(dst[2]) {}
+  template <typename T>
+  HOST_DEVICE bool operator()(const T* const pose, T* residuals) const {
+    const T s[3] = {T(sx), T(sy), T(sz)};
+    T q[3];
+    AngleAxisRotatePoint(pose, s, q);
+    residuals[0] = q[0] + pose[3] - tx;
+    residuals[1] = q[1] + pose[4] - ty;
+    residuals[2] = q[2] + pose[5] - tz;
+    return true;
+  }
+  double sx, sy, sz, tx, ty, tz;
+};
+
 // SoftLOneLoss (internal/ceres/loss_function.cc:66-73) as a LossFunctionCUDA.
 class SoftLOneLossCUDA {
  public:

@@ -14,6 +14,8 @@
 //   BinaryScalarCost,          internal/ceres/autodiff_cost_function_cuda_test.cu.cc:
 //   TenParameterCost,          40-51, 123-139, 224-230
 //   OnlyFillsOneOutputFunctor
+// three functors of other shapes (PoseReprojectionError <2, 6, 3> with six
+// doubles of data, PointToPlaneError <1, 6, 3>, RigidAlignmentError <3, 6>),
 // and two losses of internal/ceres/loss_function.cc as LossFunctionCUDA
 // classes: SoftLOneLoss (:66-73) and TolerantLoss (:93-118, rho'' > 0: the
 // Corrector's full branch).
@@ -52,6 +54,10 @@ const Entry kEntries[] = {
     {"TenParameterCost/Trivial",
      &Reg<user::TenParameterCost, TrivialLossCUDA, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1>},
     {"OnlyFillsOneOutputFunctor/Trivial", &Reg<user::OnlyFillsOneOutputFunctor, TrivialLossCUDA, 2, 1>},
+    {"PoseReprojectionError/Trivial", &Reg<user::PoseReprojectionError, TrivialLossCUDA, 2, 6, 3>},
+    {"PoseReprojectionError/Huber", &Reg<user::PoseReprojectionError, HuberLossCUDA, 2, 6, 3>},
+    {"PointToPlaneError/Cauchy", &Reg<user::PointToPlaneError, CauchyLossCUDA, 1, 6, 3>},
+    {"RigidAlignmentError/Trivial", &Reg<user::RigidAlignmentError, TrivialLossCUDA, 3, 6>},
 };
 constexpr int kNumEntries = (int)(sizeof(kEntries) / sizeof(kEntries[0]));
 

@@ -17,12 +17,15 @@ NAMES = {
     "PointDisplacementError/Trivial": (3, (3,), 3),
     "BinaryScalarCost/Trivial": (1, (2, 2), 1),
     "TenParameterCost/Trivial": (1, (1,) * 10, 1),
+    "PoseReprojectionError/Trivial": (2, (6, 3), 6),
+    "PointToPlaneError/Cauchy": (1, (6, 3), 4),
+    "RigidAlignmentError/Trivial": (3, (6,), 6),
 }
 
 
 def test_registration_shapes_and_idempotence():
     lib, kinds = U.library()
-    assert len(kinds) == 13
+    assert len(kinds) == 17
     assert all(k >= _cse.FUNCTOR_USER_FIRST for k in kinds.values())
     assert len(set(kinds.values())) == len(kinds)
     for name, shape in NAMES.items():

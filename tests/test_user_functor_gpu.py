@@ -247,3 +247,105 @@ def test_user_kind_on_a_multi_device_evaluator(gpu):
         ev.close()
     assert np.array_equal(one[2], multi[2]) and np.array_equal(one[4], multi[4])
     assert_parity(multi, one, "multi-device user kind")
+
+
+# ---- Shapes outside the library's kinds on the affine kernels --------------
+# PoseReprojectionError <2, 6, 3> (six doubles of functor data),
+# PointToPlaneError <1, 6, 3>, RigidAlignmentError <3, 6> (examples/
+# user_functors.h): each runs the affine kernels (cse::kAffineShape) and is
+# checked against the general kernel, which evaluates the same functor one
+# block per lane through the offset tables -- residuals, Jacobian (both
+# layouts), cost, gradient, and the Jacobian operators.
+
+def _scene(C, P, per_point, seed):
+    rng = np.random.default_rng(seed)
+    poses = np.concatenate([rng.normal(0, 0.05, (C, 3)),
+                            np.stack([rng.normal(0, 1, C), rng.normal(0, 1, C),
+                                      -10 + rng.normal(0, 1, C)], axis=1)], axis=1)
+    pts = rng.uniform(-3, 3, (P, 3))
+    ci = np.concatenate([rng.permutation(C)[:per_point] for _ in range(P)]).astype(np.int32)
+    pi = np.repeat(np.arange(P, dtype=np.int32), per_point)
+    return rng, poses, pts, ci, pi
+
+
+def _pose_point_problem(name, seed=3, C=40, P=3000, per_point=5):
+    """Points first (the Schur elimination group), then poses; residual
+    blocks point-major, as bundle_adjuster orders them."""
+    rng, poses, pts, ci, pi = _scene(C, P, per_point, seed)
+    pb = ca.ProblemCUDA()
+    pid = [pb.add_parameter_block(p) for p in pts]
+    cid = [pb.add_parameter_block(c) for c in poses]
+    ids = np.stack([np.asarray(cid)[ci], np.asarray(pid)[pi]], axis=1)
+    n = len(ci)
+    if name.startswith("PoseReprojectionError"):
+        # u, v from the model plus noise; fx, fy, cx, cy per observation
+        intr = np.stack([rng.uniform(400, 600, n), rng.uniform(400, 600, n),
+                         rng.uniform(300, 340, n), rng.uniform(220, 260, n)], axis=1)
+        uv = rng.normal(320, 50, (n, 2))
+        data = np.concatenate([uv, intr], axis=1)
+        loss = ca.Loss.huber(1.0) if name.endswith("Huber") else None
+    else:  # PointToPlaneError
+        nrm = rng.normal(size=(n, 3))
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        data = np.concatenate([nrm, rng.normal(0, 2, (n, 1))], axis=1)
+        loss = ca.Loss.cauchy(2.0)
+    pb.add_residual_blocks(U.kind(name), loss, ids, data)
+    return pb, P
+
+
+def _rigid_problem(seed=5, C=64, per_pose=400):
+    rng = np.random.default_rng(seed)
+    pb = ca.ProblemCUDA()
+    poses = np.concatenate([rng.normal(0, 0.1, (C, 3)), rng.normal(0, 1, (C, 3))], axis=1)
+    cid = [pb.add_parameter_block(c) for c in poses]
+    n = C * per_pose
+    ids = np.repeat(np.asarray(cid, np.int32), per_pose)[:, None]
+    data = np.concatenate([rng.uniform(-5, 5, (n, 3)), rng.uniform(-5, 5, (n, 3))], axis=1)
+    pb.add_residual_blocks(U.kind("RigidAlignmentError/Trivial"), None, ids, data)
+    return pb, 0
+
+
+def _close(a, b, tol=1e-13):
+    return np.linalg.norm(a - b) <= tol * max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+@pytest.mark.parametrize("name", ["PoseReprojectionError/Trivial", "PoseReprojectionError/Huber",
+                                  "PointToPlaneError/Cauchy", "RigidAlignmentError/Trivial"])
+def test_other_shapes_on_the_affine_kernels(gpu, name, fmt):
+    pb, n_elim = (_rigid_problem() if name.startswith("Rigid") else _pose_point_problem(name))
+    prog = pb.program()
+    prog.compile(fmt, num_eliminate_blocks=n_elim if fmt == ca.BLOCK_SPARSE else 0)
+    fast, info_f = evaluate(prog)
+    gen, info_g = evaluate(prog, force_general_layout=True)
+    assert info_f.num_affine_groups == 1 and info_g.num_affine_groups == 0, name
+    assert fast[0] and gen[0]
+    assert abs(fast[1] - gen[1]) <= 1e-13 * abs(gen[1]), (name, fast[1], gen[1])
+    for k, what in ((2, "residuals"), (3, "gradient"), (4, "jacobian")):
+        assert np.isfinite(fast[k]).all(), (name, what)
+        assert _close(fast[k], gen[k]), (name, what, np.linalg.norm(fast[k] - gen[k]))
+    # residual-only and cost-only kernels of the shape
+    r_only, _ = evaluate(prog, residuals=True, gradient=False, jacobian=False)
+    assert _close(r_only[2], gen[2]) and abs(r_only[1] - gen[1]) <= 1e-13 * abs(gen[1])
+    # J x and J^T x of the affine group against the dense Jacobian
+    from test_spmv_gpu import dense_jacobian
+    J = dense_jacobian(prog, gen[4])
+    rng = np.random.default_rng(1)
+    x = rng.normal(size=prog.num_effective_parameters)
+    z = rng.normal(size=prog.num_residuals)
+    import torch
+    dev = torch.device("cuda", 0)
+    ev = ca.Evaluator(prog, stream=torch.cuda.current_stream(dev).cuda_stream)
+    try:
+        dj = torch.from_numpy(fast[4]).to(dev)
+        dx, dz = torch.from_numpy(x).to(dev), torch.from_numpy(z).to(dev)
+        y = torch.zeros(prog.num_residuals, dtype=torch.float64, device=dev)
+        w = torch.zeros(prog.num_effective_parameters, dtype=torch.float64, device=dev)
+        ev.evaluate()  # the operators' plans
+        ev.right_multiply_device(dj.data_ptr(), dx.data_ptr(), y.data_ptr())
+        ev.left_multiply_device(dj.data_ptr(), dz.data_ptr(), w.data_ptr())
+        torch.cuda.synchronize(dev)
+    finally:
+        ev.close()
+    assert _close(y.cpu().numpy(), J @ x, 1e-12), name
+    assert _close(w.cpu().numpy(), J.T @ z, 1e-12), name

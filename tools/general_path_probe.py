@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The general (table) kernel against the affine fast path on one problem.
 
-Every functor shape outside the affine-validated set (user functors of other
+Every functor shape the affine kernels do not take (user functors of other
 shapes, manifolds given as explicit plus-Jacobians, ...) runs
 EvaluateTableKernel.  This times both paths on the same BAL-shaped Program
 (cse_options.force_general_layout), device-resident residuals + Jacobian +
