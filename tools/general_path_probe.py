@@ -34,10 +34,32 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--lib", default=None, help="load this build of libcse.so")
+    ap.add_argument("--pose-reprojection", action="store_true",
+                    help="the user functor PoseReprojectionError <2, 6, 3> of examples/"
+                         "user_functors.hip (6-parameter poses, intrinsics in the functor) "
+                         "on the same BAL structure, Huber")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
-    prog = bal.synthetic_program(args.config, loss=ca.Loss.huber(1.0), format=args.format)
+    if args.pose_reprojection:
+        import ctypes as C
+        from ceres_amd import _cse
+        lib = _cse.load_functor_library(os.path.join(REPO, "examples", "build",
+                                                     "libuser_functors.so"))
+        lib.cse_example_kind_name.restype = C.c_char_p
+        kinds = (C.c_int32 * 64)()
+        n = lib.cse_example_register(kinds, 64)
+        kind = {lib.cse_example_kind_name(i).decode(): kinds[i] for i in range(n)}[
+            "PoseReprojectionError/Huber"]
+        cams, pts, ci, pi, obs = bal.synthetic(*bal.CONFIGS[args.config])
+        m = len(ci)
+        data = np.empty((m, 6))
+        data[:, :2] = obs
+        data[:, 2:] = (500.0, 500.0, 0.0, 0.0)
+        prog = bal.program(np.ascontiguousarray(cams[:, :6]), pts, ci, pi, data, kind=kind,
+                           loss=ca.Loss.huber(1.0), format=args.format)
+    else:
+        prog = bal.synthetic_program(args.config, loss=ca.Loss.huber(1.0), format=args.format)
     f64 = torch.float64
     state = torch.from_numpy(prog.state).to(dev)
     out = {}
@@ -71,6 +93,11 @@ def main():
     out["rel_diff"] = {"cost": abs(float(a[0] - t[0])) / abs(float(t[0])),
                        "residuals": rel(a[1], t[1]), "jacobian": rel(a[2], t[2])}
     out["config"] = args.config
+    out["functor"] = "PoseReprojectionError<2,6,3> (user)" if args.pose_reprojection else "Snavely<2,9,3>"
+    # algorithmic bytes of the affine evaluation (cse_info), for its HBM rate
+    info = evs["affine"].info()
+    out["affine_bytes"] = info.bytes_jacobian_eval
+    out["affine_GBps"] = info.bytes_jacobian_eval / (out["affine"]["ms_per_eval"] * 1e-3) / 1e9
     out["format"] = args.format
     for ev in evs.values():
         ev.close()
