@@ -1446,6 +1446,164 @@ __global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsKernel(const int
   sid1[q] = ids[2 * b + 1];
 }
 
+// The general kernel's output stores, for the whole wave.  When the wave's
+// rows form contiguous runs -- residuals NR apart; BlockSparseMatrix cells
+// of consecutive blocks (slot j's row k at cell + k t_j, cells NR t_j
+// apart); or CompressedRow row blocks (a block's NR rows of W = sum t_j
+// values whose slot segments tile the row, blocks NR W apart) -- the wave
+// stages the rows in LDS and stores each run with consecutive lanes on
+// consecutive doubles (one 512-byte span per store instruction instead of 64
+// scattered rows; the scatter made the kernel L2-request bound, 5.9x the
+// affine kernel's requests, profiles/round6/r6s).  Otherwise (blocks held
+// constant in part of the wave, manifold tangent sizes that differ, other
+// layouts) each lane scatters its rows through the offset tables as
+// WriteJacobians does (cuda_evaluator_kernel.h:260-294).  A failed block's
+// outputs are unspecified (the evaluation reports the failure), so the
+// staged runs carry them along.
+template <class K>
+constexpr bool kTableStaged = KindTraits<K>::NR * KindTraits<K>::N <= 32;
+
+template <class K, bool kJac>
+__device__ __forceinline__ void TableStores(const GroupArgs& a, bool active, bool ok, int64_t gi,
+                                            const PbDev* pb, const double* r, const double* J,
+                                            double* st) {
+  using Tr = KindTraits<K>;
+  constexpr int NR = Tr::NR, NB = Tr::NB, N = Tr::N;
+  constexpr bool kStaged = kTableStaged<K>;
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t act = __ballot(active);
+  if (act == 0) return;
+  const int nb = __popcll(act);  // the active lanes are a prefix of the wave
+  // Every active lane satisfies c (wave-uniform).
+  auto all = [&](bool c) { return __ballot(active && !c) == 0; };
+  auto sync = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (a.residuals) {
+    const int64_t off = active ? a.residual_layout[gi] : 0;
+    const int64_t off0 = __shfl(off, 0, kWave);
+    if (kStaged && all(off == off0 + (int64_t)NR * lane)) {
+      if (active) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
+      }
+      sync();
+      for (int p = lane; p < nb * NR; p += kWave) a.residuals[off0 + p] = st[p];
+      sync();
+    } else if (active && ok) {
+#pragma unroll
+      for (int k = 0; k < NR; ++k) a.residuals[off + k] = r[k];
+    }
+  }
+  if constexpr (kJac) {
+    if (!a.jacobian) return;
+    // Row (j, k) of slot j's a-th active position goes to
+    // values + offsets[layout[gi] + a NR + k].
+    const int64_t q = active ? a.jac_layout[gi] : 0;
+    bool uniform = kStaged;
+    bool cst[NB];
+    int t[NB];
+    int64_t row[NB][NR];
+    int na = 0;  // active slots (wave-uniform when `uniform`)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const bool c = active && pb[j].is_constant;
+      const uint64_t m = __ballot(c);
+      cst[j] = m != 0;
+      uniform = uniform && (m == 0 || m == act);
+      t[j] = __shfl(active ? pb[j].tangent_size : 0, 0, kWave);
+      uniform = uniform && all(pb[j].is_constant || pb[j].tangent_size == t[j]);
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+        row[j][k] = active && !cst[j] ? a.jac_offsets[q + (int64_t)na * NR + k] : 0;
+      if (!cst[j]) ++na;
+    }
+    bool bsm = uniform, crs = uniform;
+    int64_t base[NB];
+    int64_t r0 = INT64_MAX;
+    int w = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      base[j] = __shfl(row[j][0], 0, kWave);
+      if (cst[j]) continue;
+      r0 = base[j] < r0 ? base[j] : r0;
+      w += t[j];
+    }
+    if (uniform) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (cst[j]) continue;
+        bool b = true, c = true;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          b = b && row[j][k] == base[j] + (int64_t)lane * NR * t[j] + (int64_t)k * t[j];
+          c = c && row[j][k] == base[j] + (int64_t)lane * NR * w + (int64_t)k * w;
+        }
+        bsm = bsm && all(b);
+        crs = crs && all(c);
+        // CompressedRow: the slot segments [base - r0, + t) tile [0, w)
+        const int64_t cj = base[j] - r0;
+        crs = crs && cj >= 0 && cj + t[j] <= w;
+#pragma unroll
+        for (int j2 = 0; j2 < j; ++j2) {
+          if (cst[j2]) continue;
+          const int64_t c2 = base[j2] - r0;
+          crs = crs && (cj + t[j] <= c2 || c2 + t[j2] <= cj);
+        }
+      }
+    }
+    if (bsm) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (cst[j]) continue;
+        const int cell = NR * t[j];
+        if (active) {
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int c = 0; c < Tr::Size(j); ++c)
+              if (c < t[j]) st[lane * cell + k * t[j] + c] = J[k * N + Tr::Off(j) + c];
+        }
+        sync();
+        for (int p = lane; p < nb * cell; p += kWave) a.jacobian[base[j] + p] = st[p];
+        sync();
+      }
+    } else if (crs) {
+      const int blk = NR * w;
+      if (active) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if (cst[j]) continue;
+          const int cj = (int)(base[j] - r0);
+#pragma unroll
+          for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int c = 0; c < Tr::Size(j); ++c)
+              if (c < t[j]) st[lane * blk + k * w + cj + c] = J[k * N + Tr::Off(j) + c];
+        }
+      }
+      sync();
+      for (int p = lane; p < nb * blk; p += kWave) a.jacobian[r0 + p] = st[p];
+      sync();
+    } else if (active && ok) {
+      int64_t qq = q;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (pb[j].is_constant) continue;
+        const int tj = pb[j].tangent_size;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+          double* dst = a.jacobian + a.jac_offsets[qq++];
+#pragma unroll
+          for (int c = 0; c < Tr::Size(j); ++c)
+            if (c < tj) dst[c] = J[k * N + Tr::Off(j) + c];
+        }
+      }
+    }
+  }
+}
+
 // The general (table) path for any kind, any number of parameter blocks;
 // also runs affine groups when force_general_layout is set.  One block per
 // lane, one launch-wide grid.  Per block, as ResidualBlock::Evaluate
@@ -1456,29 +1614,30 @@ __global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsKernel(const int
 // plus-Jacobian for manifold blocks, loss and Corrector, gradient atomics,
 // residuals and Jacobian rows scattered through the offset tables
 // (WriteJacobians, :260-294).
-// waves_per_eu(2, 2): at the default occupancy target the compiler keeps
-// the local Jacobian (NR x N doubles) in scratch (208 bytes a lane for
-// Snavely); with the register budget of two waves it lives in 126 VGPRs
-// (the hardware still fits four waves) and the general path of
-// problem-1778 BSM goes from 1.108 to 0.799 ms (profiles/round6/r6o).
+// The local Jacobian (NR x N doubles) stays in registers: every index into
+// it is a compile-time constant once the loops unroll (a `break` on the
+// runtime tangent size in the gradient loop used to leave it in 208 bytes of
+// scratch a lane; profiles/round6/r6o).  Outputs: TableStores.
 template <class K, int kLoss, bool kJac>
-__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void
-EvaluateTableKernel(const GroupArgs a) {
+__global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const GroupArgs a) {
   using Tr = KindTraits<K>;
   constexpr int NR = Tr::NR, NB = Tr::NB, N = Tr::N, D = Tr::D;
   static_assert(NB <= kMaxSlots, "too many parameter blocks");
 
   const int64_t i = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
   const bool active = i < a.n;
-  const bool want_jac = kJac && a.jacobian != nullptr;
   const bool want_grad = kJac && a.gradient != nullptr;
   double cost = 0.0;
+  __shared__ double stage_all[kWavesPerBlock][kTableStaged<K> ? kWave * NR * N : 1];
+  PbDev pb[NB] = {};
+  double r[NR], J[NR * N];
+  bool ok = false;
+  int64_t gi = 0;
 
   if (active) {
     double d[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) d[k] = a.data[i * D + k];
-    PbDev pb[NB];
     double x[N];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -1487,8 +1646,7 @@ EvaluateTableKernel(const GroupArgs a) {
 #pragma unroll
       for (int c = 0; c < Tr::Size(j); ++c) x[Tr::Off(j) + c] = p[c];
     }
-    double r[NR], J[NR * N];
-    bool ok = EvaluateFunctorFlat<K, kJac>(d, x, r, J);
+    ok = EvaluateFunctorFlat<K, kJac>(d, x, r, J);
     if (ok && a.check_finite) {
       bool bad = AnyNonFinite<NR>(r);
       if constexpr (kJac) bad = bad || AnyNonFinite<NR * N>(J);
@@ -1585,41 +1743,23 @@ EvaluateTableKernel(const GroupArgs a) {
           if (pb[j].is_constant) continue;
           double* g = a.gradient + pb[j].delta_offset;
           const int t = pb[j].tangent_size;
+          // (c < t as a guard, not a break: the loop unrolls fully and J
+          // stays in registers)
 #pragma unroll
           for (int c = 0; c < Tr::Size(j); ++c) {
-            if (c >= t) break;
-            double s = 0.0;
+            if (c < t) {
+              double s = 0.0;
 #pragma unroll
-            for (int k = 0; k < NR; ++k) s += J[k * N + Tr::Off(j) + c] * r[k];
-            unsafeAtomicAdd(g + c, s);
-          }
-        }
-      }
-      const int64_t gi = a.gindex ? a.gindex[i] : a.first + i;
-      if (a.residuals) {
-        double* dst = a.residuals + a.residual_layout[gi];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) dst[k] = r[k];
-      }
-      if (want_jac) {
-        // WriteJacobians (cuda_evaluator_kernel.h:260-294): row k of the
-        // a-th active slot goes to values + offsets[layout[gi] + a*kR + k].
-        int64_t q = a.jac_layout[gi];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if (pb[j].is_constant) continue;
-          const int t = pb[j].tangent_size;
-#pragma unroll
-          for (int k = 0; k < NR; ++k) {
-            double* dst = a.jacobian + a.jac_offsets[q++];
-#pragma unroll
-            for (int c = 0; c < Tr::Size(j); ++c)
-              if (c < t) dst[c] = J[k * N + Tr::Off(j) + c];
+              for (int k = 0; k < NR; ++k) s += J[k * N + Tr::Off(j) + c] * r[k];
+              unsafeAtomicAdd(g + c, s);
+            }
           }
         }
       }
     }
+    gi = a.gindex ? a.gindex[i] : a.first + i;
   }
+  TableStores<K, kJac>(a, active, ok, gi, pb, r, J, stage_all[threadIdx.x / kWave]);
   // One partial per wave (the wave's 64 blocks are the affine kernels'
   // chunk, so both paths sum the same partials in the same order).
   const double w = WaveSumLane0(cost);
