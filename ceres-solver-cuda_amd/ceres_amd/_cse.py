@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libcse.so"))
 
-CSE_ABI_VERSION = 4
+CSE_ABI_VERSION = 5
 
 # cse_options.jacobian_form (cse_jacobian_form)
 JACOBIAN_CLOSED_FORM = 0

@@ -364,6 +364,30 @@ bool FusedKind(int kind) {
   return kind == CSE_FUNCTOR_SNAVELY_2_9_3 || kind == kKindQuaternionTangent;
 }
 
+// f(std::integral_constant<int, s0>) for the slot-0 sizes the fused
+// gradient's tail is built for (1..16, the affine kernels' bound).
+template <class F>
+bool VisitSlot0Size(int s0, F&& f) {
+  switch (s0) {
+#define CSE_S0_CASE(n) \
+  case n: f(std::integral_constant<int, n>{}); return true;
+    CSE_S0_CASE(1) CSE_S0_CASE(2) CSE_S0_CASE(3) CSE_S0_CASE(4) CSE_S0_CASE(5) CSE_S0_CASE(6)
+    CSE_S0_CASE(7) CSE_S0_CASE(8) CSE_S0_CASE(9) CSE_S0_CASE(10) CSE_S0_CASE(11) CSE_S0_CASE(12)
+    CSE_S0_CASE(13) CSE_S0_CASE(14) CSE_S0_CASE(15) CSE_S0_CASE(16)
+#undef CSE_S0_CASE
+    default: return false;
+  }
+}
+
+// User kinds that registered the fused gradient's launches (cse_functor_ops
+// ABI 5: two slots, slot 1 of 3 parameters): gradient_mode 0's form only
+// (points kernel, CameraGradientKernel, the tail); the other modes, the Jet
+// form and the operators stay with the library's kinds.
+bool UserFused(const Group& G) {
+  return G.user && G.user->fused_points[0] && G.user->fused_points[1] && G.user->camera_gradient &&
+         G.shape.nb == 2 && G.shape.s1 == 3 && G.shape.s0 >= 1 && G.shape.s0 <= 16;
+}
+
 template <class K>
 LaunchFn PickFusedK(int loss, bool crs, bool points) {
   switch (loss) {
@@ -1076,13 +1100,17 @@ int CamGradSortedInputs(Group& G, hipStream_t s) {
   const int D = G.shape.data;
   int rc;
   if (!G.sorted_ready) {  // set only once the copies have been queued
-    if (D != 2) return Fail(CSE_ERR_UNSUPPORTED, "camera-order gradient: 2 data doubles per block");
+    if (D != 2 && !UserFused(G))
+      return Fail(CSE_ERR_UNSUPPORTED, "camera-order gradient: 2 data doubles per block");
     if ((rc = G.sdata.alloc((size_t)G.n * D))) return rc;
     if ((rc = G.sid1.alloc((size_t)G.n))) return rc;
-    hipLaunchKernelGGL((cse::SortSlot0InputsKernel<2>),
-                       dim3((unsigned)((G.n + cse::kBlockThreads - 1) / cse::kBlockThreads)),
-                       dim3(cse::kBlockThreads), 0, s, G.ids.p, G.data.p, P.perm.p, P.nperm, G.sdata.p,
-                       G.sid1.p);
+    const dim3 grid((unsigned)((G.n + cse::kBlockThreads - 1) / cse::kBlockThreads));
+    if (D == 2)
+      hipLaunchKernelGGL((cse::SortSlot0InputsKernel<2>), grid, dim3(cse::kBlockThreads), 0, s, G.ids.p,
+                         G.data.p, P.perm.p, P.nperm, G.sdata.p, G.sid1.p);
+    else
+      hipLaunchKernelGGL((cse::SortSlot0InputsAnyKernel<>), grid, dim3(cse::kBlockThreads), 0, s, G.ids.p,
+                         G.data.p, D, P.perm.p, P.nperm, G.sdata.p, G.sid1.p);
     CSE_HIP(hipGetLastError());
     G.sorted_ready = true;
   }
@@ -1115,6 +1143,13 @@ int LaunchCameraGradKernel(cse_evaluator* ev, Group& G, const double* state, hip
     cg.packed0 = G.packed0.p;
     cg.packed_lo = G.slot0_lo;
     cg.packed_stride = G.packed_stride;
+  }
+  if (G.user) {  // the kind's own CameraGradientKernel (its TU), with its loss object
+    static_assert(sizeof(cg.user_loss) == sizeof(G.loss.user), "user loss bytes");
+    std::memcpy(cg.user_loss, G.loss.user, sizeof(cg.user_loss));
+    if (P.nchunks > 0) G.user->camera_gradient(&cg, cg.nslots, s);
+    CSE_HIP(hipGetLastError());
+    return CSE_OK;
   }
   constexpr int W = kCamGradWavesPerWg;
   const dim3 grid((unsigned)((cg.nslots + W - 1) / W));
@@ -1160,12 +1195,17 @@ int LaunchCameraGradReduce(Group& G, double* out, hipStream_t s, bool assign = f
   const cse::GradChunks ch{P.chunk_begin.p, P.chunk_off.p, P.chunk_partial.p, P.nchunks};
   const int64_t cwg = (ga.count + cse::kBlockThreads - 1) / cse::kBlockThreads;
   const dim3 grid((unsigned)(bwg + cwg));
-  if (assign)
-    hipLaunchKernelGGL((cse::GradientTailKernel<3, 9, true>), grid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
-                       entries, G.delta_base[1], bwg, ga, ch);
-  else
-    hipLaunchKernelGGL((cse::GradientTailKernel<3, 9, false>), grid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
-                       entries, G.delta_base[1], bwg, ga, ch);
+  auto tail = [&](auto s0) {
+    constexpr int S0 = decltype(s0)::value;
+    if (assign)
+      hipLaunchKernelGGL((cse::GradientTailKernel<3, S0, true>), grid, dim3(cse::kBlockThreads), 0, s, G.gside.p,
+                         entries, G.delta_base[1], bwg, ga, ch);
+    else
+      hipLaunchKernelGGL((cse::GradientTailKernel<3, S0, false>), grid, dim3(cse::kBlockThreads), 0, s,
+                         G.gside.p, entries, G.delta_base[1], bwg, ga, ch);
+  };
+  if (!VisitSlot0Size(G.shape.s0, tail))
+    return Fail(CSE_ERR_UNSUPPORTED, "fused gradient: slot 0 of " + std::to_string(G.shape.s0) + " parameters");
   CSE_HIP(hipGetLastError());
   return CSE_OK;
 }
@@ -1255,7 +1295,8 @@ GradPath GradPathOf(const cse_evaluator* ev, const Group& G, bool grad, bool res
   // constant slot-0 blocks: it takes mode 0's fused form (also fixed order).
   // The Jet form has no mode-3 kernel (contributions in block order): the
   // post-pass instead, as for groups without a fused form.
-  p.fused = p.grad_pass && G.fuse_ok && (mode == 0 || (mode == 3 && !G.jet) || (mode == 1 && G.const0));
+  p.fused = p.grad_pass && G.fuse_ok &&
+            (mode == 0 || (!G.user && ((mode == 3 && !G.jet) || (mode == 1 && G.const0))));
   // Constant slot-0 blocks: no post-pass over the packed F cells (in-kernel
   // atomics instead, active cameras only).
   if (G.const0 && !p.fused) p.grad_pass = false;
@@ -1332,7 +1373,10 @@ int Enqueue(cse_evaluator* ev, const double* d_state, double* d_cost, double* d_
       a.gfused = d_grad;
       a.gside = G.gside.p;
       a.gcontrib = G.gcontrib.p;
-      fn = PickFused(G.kind, G.loss.kind, G.policy, recompute, G.const0);
+      if (G.user)
+        ufn = G.user->fused_points[G.policy == kAffineCrs];
+      else
+        fn = PickFused(G.kind, G.loss.kind, G.policy, recompute, G.const0);
       if (G.jet) fn = cse::JetSnavelyFusedPoints(G.loss.kind, G.policy == kAffineCrs);
     }
     if (timing.first && g == 0) CSE_HIP(hipEventRecord(timing.first, ev->stream));
@@ -1700,7 +1744,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
         if (GradSupported(k.nr, sizes[j], G.user, j) &&
             (rc = BuildGradPlan(g, k, j, &G.grad[j], s,
                                 j == 0 && G.const0 ? d->parameter_blocks : nullptr,
-                                j == 0 && k.nb == 2 && FusedKind(G.kind) ? CamGradPasses(g, k) : 1)))
+                                j == 0 && k.nb == 2 && (FusedKind(G.kind) || UserFused(G))
+                                    ? CamGradPasses(g, k)
+                                    : 1)))
           return bail(rc);
     }
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
@@ -1717,7 +1763,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
   // and whose slot-0 blocks have a chunked plan.
   for (int gi = 0; gi < (int)ev->groups.size(); ++gi) {
     Group& G = ev->groups[gi];
-    bool ok = FusedKind(G.kind) && G.affine && G.n > 0 && G.packed0.p &&
+    bool ok = (FusedKind(G.kind) || UserFused(G)) && G.affine && G.n > 0 && G.packed0.p &&
               G.grad[0].ready && G.grad[0].perm.p && G.grad[0].nchunks > 0 && G.grad[1].ready &&
               G.grad[1].perm.p == nullptr;
     const cse_residual_group& g = d->groups[gi];
@@ -1725,9 +1771,9 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
       ok = owner[g.parameter_block_ids[2 * i + 1]] == 2 * gi + 1;
     G.fuse_ok = ok;
     G.grad_exact = ok && ev->groups.size() == 1 && d->num_groups == 1 && !G.const0 &&
-                   ev->num_constant == 0 && G.shape.s0 == 9 && G.shape.s1 == 3 &&
-                   G.grad[0].all_present && G.grad[1].all_present &&
-                   9 * G.grad[0].count + 3 * G.grad[1].count == ev->num_effective;
+                   ev->num_constant == 0 && G.shape.s1 == 3 && G.grad[0].all_present &&
+                   G.grad[1].all_present &&
+                   G.shape.s0 * G.grad[0].count + 3 * G.grad[1].count == ev->num_effective;
   }
   if ((rc = BuildSchurPlan(ev, d, s))) return bail(rc);
   ev->res_covered = covered_res == d->num_residuals;
@@ -1950,7 +1996,7 @@ int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const 
                        dim3((unsigned)((ev->num_effective + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                        dim3(cse::kBlockThreads), 0, s, d_D, d_x, d_y, ev->num_effective);
   bool fused = true;
-  for (auto& G : ev->groups) fused = fused && (G.n == 0 || (G.fuse_ok && !G.const0));
+  for (auto& G : ev->groups) fused = fused && (G.n == 0 || (G.fuse_ok && !G.const0 && FusedKind(G.kind)));
   if (!fused) {
     // z = J x, then y += J^T z: the two products of CudaCgnrLinearOperator.
     int rc;
@@ -2355,7 +2401,7 @@ int cse_host_register(void* p, size_t bytes) { return CseHostRegister(p, bytes);
 int cse_host_unregister(void* p) { return CseHostUnregister(p); }
 
 // Registration compares whole tables bytewise: no padding inside.
-static_assert(offsetof(cse_functor_ops, kernel_args_tag) == 80 && sizeof(cse_functor_ops) == 200,
+static_assert(offsetof(cse_functor_ops, kernel_args_tag) == 80 && sizeof(cse_functor_ops) == 224,
               "cse_functor_ops layout");
 
 int cse_register_functor(const cse_functor_ops* ops, int32_t* kind) {
@@ -2371,6 +2417,12 @@ int cse_register_functor(const cse_functor_ops* ops, int32_t* kind) {
     return Fail(CSE_ERR_INVALID, "functor " + name +
                                      ": kernel argument layout differs from the library's (build "
                                      "the functor against the same ceres-solver-cuda_amd headers)");
+  const bool fused = ops->fused_points[0] || ops->fused_points[1] || ops->camera_gradient;
+  if (fused && (!ops->fused_points[0] || !ops->fused_points[1] || !ops->camera_gradient ||
+                ops->camera_gradient_args_size != (int32_t)sizeof(cse::CamGradArgs)))
+    return Fail(CSE_ERR_INVALID, "functor " + name +
+                                     ": the fused gradient's launches come as all three, with the "
+                                     "library's camera-gradient argument size");
   const int nb = ops->num_parameter_blocks;
   if (ops->num_residuals < 1 || nb < 1 || nb > CSE_MAX_PARAMETER_BLOCKS || ops->data_size < 1)
     return Fail(CSE_ERR_INVALID, "functor " + name + ": bad shape");
@@ -2390,6 +2442,10 @@ int cse_register_functor(const cse_functor_ops* ops, int32_t* kind) {
   if (any_affine && (!UserAffine(ops) || nb > 2 || ops->num_residuals > 3))
     return Fail(CSE_ERR_INVALID, "functor " + name + ": affine kernels must come as all eight, "
                                                      "for at most two blocks and three residuals");
+  if (fused && (!any_affine || nb != 2 || ops->parameter_block_sizes[1] != 3 ||
+                ops->parameter_block_sizes[0] > 16))
+    return Fail(CSE_ERR_INVALID, "functor " + name + ": the fused gradient is for affine kinds of two "
+                                                     "blocks, the second of 3 parameters");
   std::lock_guard<std::mutex> lock(g_user_mu);
   for (size_t i = 0; i < g_user_kinds.size(); ++i) {
     const UserKindEntry& e = *g_user_kinds[i];
@@ -2433,8 +2489,9 @@ int cse_get_info(cse_evaluator* ev, cse_info* info) {
   for (auto& G : ev->groups) {
     info->num_affine_groups += G.affine ? 1 : 0;
     info->num_fused_gradient_groups +=
-        (G.fuse_ok && (ev->opts.gradient_mode == 0 || (ev->opts.gradient_mode == 3 && !G.jet) ||
-                       (ev->opts.gradient_mode == 1 && G.const0)))
+        (G.fuse_ok && (ev->opts.gradient_mode == 0 ||
+                       (!G.user && ((ev->opts.gradient_mode == 3 && !G.jet) ||
+                                    (ev->opts.gradient_mode == 1 && G.const0)))))
             ? 1
             : 0;
   }

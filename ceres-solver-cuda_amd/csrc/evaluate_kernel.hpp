@@ -1317,6 +1317,7 @@ struct CamGradArgs {
   const double* packed0;
   int32_t packed_lo;
   int32_t packed_stride;
+  double user_loss[kUserLossDoubles];  // a user kind's loss object (kLossUser)
 };
 
 // r and the slot-0 Jacobian (NR x S0, row-major) of one block, the slot-1
@@ -1408,7 +1409,7 @@ CameraGradientKernel(const CamGradArgs g) {
       EvaluateSlot0<K>(d[u], x0, x1[u], r, J0);
 #pragma unroll
       for (int k = 0; k < NR * S1p; ++k) J1[k] = 0.0;
-      LossAndCorrect<K, kLoss, true>(g.loss, g.apply_loss, r, J0, J1);
+      LossAndCorrect<K, kLoss, true>(g.loss, g.apply_loss, r, J0, J1, true, g.user_loss);
       if (live[u]) {
 #pragma unroll
         for (int c = 0; c < S0; ++c) {
@@ -1442,6 +1443,19 @@ __global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsKernel(const int
   if (q >= n) return;
   const int64_t b = perm[q];
 #pragma unroll
+  for (int k = 0; k < D; ++k) sdata[q * D + k] = data[b * D + k];
+  sid1[q] = ids[2 * b + 1];
+}
+
+// The same for D data doubles per block (user kinds; a template so that
+// every TU including this header may instantiate it).
+template <int kUnused = 0>
+__global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsAnyKernel(const int32_t* ids, const double* data,
+                                                                          int D, const int32_t* perm, int64_t n,
+                                                                          double* sdata, int32_t* sid1) {
+  const int64_t q = (int64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+  if (q >= n) return;
+  const int64_t b = perm[q];
   for (int k = 0; k < D; ++k) sdata[q * D + k] = data[b * D + k];
   sid1[q] = ids[2 * b + 1];
 }

@@ -92,10 +92,10 @@ struct GroupArgs {
   double user_loss[kUserLossDoubles];
 };
 
-// Layout tag of GroupArgs, checked when a user functor kind registers
-// kernels compiled in another TU (cse_register_functor): bump on any change
-// to the struct.
-constexpr uint64_t kGroupArgsTag = 0x6373654761310002ull;
+// Layout tag of the argument blocks (GroupArgs, GradArgs, CamGradArgs),
+// checked when a user functor kind registers kernels compiled in another TU
+// (cse_register_functor): bump on any change to them.
+constexpr uint64_t kGroupArgsTag = 0x6373654761310003ull;
 
 // Compile-time shape of a functor kind: kR residuals, NB parameter blocks
 // of sizes kSizes[0..NB) concatenated into N columns.

@@ -108,6 +108,27 @@ void LaunchGradientSlot(const GradArgs& ga, const GradChunks& ch, int form, hipS
   }
 }
 
+// The fused gradient (gradient_mode 0) of a two-slot kind whose slot 1 has
+// 3 parameters, the form the library's Snavely kinds take: the Jacobian
+// kernel that also sums the slot-1 rows of its sorted blocks
+// (EvaluateAffineChunksFusedPointsW1, one wave per workgroup), and the
+// slot-0 rows by re-evaluation in slot-0 order (CameraGradientKernel).
+template <class K>
+constexpr bool kFusedGradShape = KindTraits<K>::NB == 2 && KindTraits<K>::S1 == 3;
+
+template <class K, int L, bool Crs>
+void LaunchFusedPointsKernel(const GroupArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((EvaluateAffineChunksFusedPointsW1<K, L, Crs>), dim3((unsigned)Chunks(a.n)), dim3(kWave),
+                     0, s, a);
+}
+
+template <class K, int L>
+void LaunchCameraGradient(const CamGradArgs& g, int64_t nslots, hipStream_t s) {
+  constexpr int W = kWavesPerBlock;
+  hipLaunchKernelGGL((CameraGradientKernel<K, L, W>), dim3((unsigned)((nslots + W - 1) / W)), dim3(W * kWave), 0,
+                     s, g);
+}
+
 }  // namespace cse
 
 #endif  // CSE_LAUNCH_HPP_

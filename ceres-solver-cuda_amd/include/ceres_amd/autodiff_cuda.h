@@ -21,7 +21,11 @@
 // at most three residuals, slot 0 at most 16 values, slot 1 at most 8) the
 // coalesced affine kernels with the LDS-DMA camera gather, their gradient
 // post-passes and J x / J^T x -- the same kernels, same settings, as a
-// built-in kind of that shape.  The Jacobian is always by Jet<double,
+// built-in kind of that shape -- and for two-block shapes whose second block
+// has 3 parameters (<NR, S0, 3>: cameras and points) the fused gradient of
+// the library's Snavely kinds (cse::kFusedGradShape: the Jacobian kernel
+// summing the point rows, CameraGradientKernel the camera rows; ABI 5).
+// The Jacobian is always by Jet<double,
 // sum Ns> (AutoDifferentiate, include/ceres/internal/autodiff.h:314-381).
 //
 // Functor requirements (as the reference's, README.md:19-50): every member
@@ -126,6 +130,16 @@ void GradientLaunch(const void* ga, const void* ch, int32_t form, void* s) {
                                  *static_cast<const cse::GradChunks*>(ch), form, (hipStream_t)s);
 }
 
+template <class K, int L, bool Crs>
+void FusedPointsLaunch(const void* a, int64_t num_wg, void* s) {
+  (void)num_wg;
+  cse::LaunchFusedPointsKernel<K, L, Crs>(Args(a), (hipStream_t)s);
+}
+template <class K, int L>
+void CameraGradientLaunch(const void* g, int64_t nslots, void* s) {
+  cse::LaunchCameraGradient<K, L>(*static_cast<const cse::CamGradArgs*>(g), nslots, (hipStream_t)s);
+}
+
 template <class K, int L>
 cse_functor_ops MakeOps(const char* name) {
   using Tr = cse::KindTraits<K>;
@@ -155,6 +169,12 @@ cse_functor_ops MakeOps(const char* name) {
     o.affine[1][1][1] = &AffineLaunch<K, L, true, true, true>;
     o.gradient[0] = &GradientLaunch<Tr::NR, K::kSizes[0]>;
     if constexpr (Tr::NB > 1) o.gradient[1] = &GradientLaunch<Tr::NR, K::kSizes[Tr::NB > 1 ? 1 : 0]>;
+    if constexpr (cse::kFusedGradShape<K>) {
+      o.fused_points[0] = &FusedPointsLaunch<K, L, false>;
+      o.fused_points[1] = &FusedPointsLaunch<K, L, true>;
+      o.camera_gradient = &CameraGradientLaunch<K, L>;
+      o.camera_gradient_args_size = (int32_t)sizeof(cse::CamGradArgs);
+    }
   }
   return o;
 }

@@ -31,8 +31,10 @@ extern "C" {
  *    shard-local state in cse_create_multi.
  * 3: cse_options.jacobian_form.
  * 4: user functor kinds (cse_register_functor, cse_functor_shape),
- *    CSE_LOSS_USER and cse_loss.user, cse_schur_init_gradient. */
-#define CSE_ABI_VERSION 4
+ *    CSE_LOSS_USER and cse_loss.user, cse_schur_init_gradient.
+ * 5: cse_functor_ops.fused_points / camera_gradient (the fused gradient for
+ *    user kinds) and camera_gradient_args_size (was reserved[0]). */
+#define CSE_ABI_VERSION 5
 
 /* Return codes. */
 #define CSE_OK 0
@@ -309,6 +311,11 @@ typedef void (*cse_multiply_launch_fn)(const void* kernel_args, int32_t which, c
  * 2 = one lane per parameter block. */
 typedef void (*cse_gradient_launch_fn)(const void* gradient_args, const void* chunks, int32_t form,
                                        void* stream);
+/* The fused gradient's slot-0 rows: one wave per chunk of a slot-0 block's
+ * residual blocks, re-evaluated in slot-0 order (camera_gradient_args ->
+ * the library's CamGradArgs); num_slots = waves to launch. */
+typedef void (*cse_camera_gradient_launch_fn)(const void* camera_gradient_args, int64_t num_slots,
+                                              void* stream);
 
 typedef struct cse_functor_ops {
   int32_t abi_version;          /* CSE_ABI_VERSION */
@@ -320,13 +327,21 @@ typedef struct cse_functor_ops {
   int32_t loss_size;            /* CSE_LOSS_USER: bytes of the loss object */
   int32_t kernel_args_size;
   int32_t gradient_args_size;
-  int32_t reserved[2];          /* 0 */
+  int32_t camera_gradient_args_size; /* with camera_gradient; else 0 */
+  int32_t reserved;             /* 0 */
   uint64_t kernel_args_tag;
   const char* name;             /* copied; for messages and cse_functor_name */
   cse_kernel_launch_fn table[2];        /* general kernel [0 residuals/cost, 1 + Jacobian] */
   cse_kernel_launch_fn affine[2][2][2]; /* [CompressedRow][Jacobian][LDS-DMA gather]; NULL = none */
   cse_multiply_launch_fn multiply;
   cse_gradient_launch_fn gradient[2];   /* per slot of an affine kind; NULL = in-kernel atomics */
+  /* ABI 5, two-slot affine kinds whose slot 1 has 3 parameters (both or
+   * neither): gradient_mode 0's fused form, as the library's Snavely kinds
+   * take it -- the Jacobian kernel that also sums the slot-1 rows
+   * [CompressedRow], and the slot-0 rows by re-evaluation.  NULL = the
+   * gradient post-passes above. */
+  cse_kernel_launch_fn fused_points[2];
+  cse_camera_gradient_launch_fn camera_gradient;
 } cse_functor_ops;
 
 /* Registers a user functor kind; *kind receives its number

@@ -42,18 +42,19 @@ def test_unknown_kind_has_no_shape():
 
 
 class functor_ops(C.Structure):
-    # include/cse.h cse_functor_ops (ABI 4), for the refusal checks only.
+    # include/cse.h cse_functor_ops (ABI 5), for the refusal checks only.
     _fields_ = [("abi_version", C.c_int32), ("num_residuals", C.c_int32),
                 ("num_parameter_blocks", C.c_int32), ("sizes", C.c_int32 * 10),
                 ("data_size", C.c_int32), ("loss_kind", C.c_int32), ("loss_size", C.c_int32),
                 ("kernel_args_size", C.c_int32), ("gradient_args_size", C.c_int32),
-                ("reserved", C.c_int32 * 2), ("kernel_args_tag", C.c_uint64),
-                ("name", C.c_char_p), ("table", C.c_void_p * 2), ("affine", C.c_void_p * 8),
-                ("multiply", C.c_void_p), ("gradient", C.c_void_p * 2)]
+                ("camera_gradient_args_size", C.c_int32), ("reserved", C.c_int32),
+                ("kernel_args_tag", C.c_uint64), ("name", C.c_char_p), ("table", C.c_void_p * 2),
+                ("affine", C.c_void_p * 8), ("multiply", C.c_void_p), ("gradient", C.c_void_p * 2),
+                ("fused_points", C.c_void_p * 2), ("camera_gradient", C.c_void_p)]
 
 
 def test_bad_launch_tables_are_refused():
-    assert C.sizeof(functor_ops) == 200
+    assert C.sizeof(functor_ops) == 224
     L = _cse.lib()
     k = C.c_int32(-1)
     o = functor_ops()

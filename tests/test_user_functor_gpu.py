@@ -89,6 +89,35 @@ def test_snavely_user_kind_equals_library_jet_kind(gpu, fmt, loss_name, loss):
 
 
 @pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+@pytest.mark.parametrize("loss_name,loss", [("Trivial", None), ("Huber", ca.Loss.huber(1.0)),
+                                            ("Cauchy", ca.Loss.cauchy(2.0))])
+def test_user_kinds_take_the_fused_gradient(gpu, fmt, loss_name, loss):
+    """ABI 5: a user kind of shape <NR, S0, 3> sums its gradient in
+    gradient_mode 0 as the library's Snavely kinds do (the points in the
+    Jacobian kernel, the camera rows by re-evaluation in camera order;
+    cse_functor_ops.fused_points / camera_gradient).  Against the same kind's
+    post-pass (mode 1) and the library kind: 1e-13; residuals and Jacobian
+    bit-equal to the post-pass run's; a repeat evaluation bit-equal; mode 3
+    (no fused form for user kinds) takes the post-pass."""
+    cams, pts, ci, pi, obs = small()
+    lib_prog = bal.program(cams, pts, ci, pi, obs, loss=loss, format=fmt)
+    user_prog = with_kind(lib_prog, U.kind("SnavelyReprojectionError/" + loss_name))
+    fused, i0 = evaluate(user_prog)
+    again, _ = evaluate(user_prog)
+    post, i1 = evaluate(user_prog, gradient_mode=1)
+    mode3, i3 = evaluate(user_prog, gradient_mode=3)
+    lib, il = evaluate(lib_prog)
+    assert i0.num_fused_gradient_groups == 1 and il.num_fused_gradient_groups == 1
+    assert i1.num_fused_gradient_groups == 0 and i3.num_fused_gradient_groups == 0
+    assert_same_bits(fused, again, (fmt, loss_name, "repeat"), gradient=True)
+    assert_same_bits(fused, post, (fmt, loss_name, "mode 1"))
+    assert np.array_equal(mode3[3], post[3]), (fmt, loss_name, "mode 3")
+    assert _close(fused[3], post[3]), np.linalg.norm(fused[3] - post[3])
+    assert _close(fused[3], lib[3]), np.linalg.norm(fused[3] - lib[3])
+    assert_parity(fused, oracle(lib_prog), (fmt, loss_name, "fused"))
+
+
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
 def test_reference_test_functors_equal_library_kinds(gpu, fmt):
     cams, pts, ci, pi, obs = small(C=12, P=500, O_=2000, seed=11)
     # SnavelyReprojectionErrorNoRadialDistortion<2, 7, 3>
@@ -201,6 +230,9 @@ def test_bundler_residual_against_the_oracle(gpu, fmt, case):
         ref = oracle(prog, kmap, lmap, **kw)
         got, info = evaluate(prog, **kw)
         assert info.num_affine_groups == 1
+        # the fused gradient (taken when residuals and Jacobian are written
+        # too), the user loss object in CameraGradientKernel's arguments
+        assert info.num_fused_gradient_groups == 1, combo
         assert_parity(got, ref, (fmt, name, combo))
     got, _ = evaluate(prog, force_general_layout=True)
     assert_parity(got, oracle(prog, kmap, lmap), (fmt, name, "general"))
@@ -222,7 +254,7 @@ def test_bundler_residual_problem_13682_full_size(gpu):
         got_r = ev.evaluate(residuals=True, gradient=False, jacobian=False)
     finally:
         ev.close()
-    assert info.num_affine_groups == 1
+    assert info.num_affine_groups == 1 and info.num_fused_gradient_groups == 1
     ref = oracle(prog, kmap, threads=16, residuals=True, gradient=True, jacobian=True)
     rep = {}
     assert_parity(got, ref, "BundlerResidual problem-13682", report=rep)
@@ -319,6 +351,9 @@ def test_other_shapes_on_the_affine_kernels(gpu, name, fmt):
     fast, info_f = evaluate(prog)
     gen, info_g = evaluate(prog, force_general_layout=True)
     assert info_f.num_affine_groups == 1 and info_g.num_affine_groups == 0, name
+    # <NR, 6, 3> with points sorted: the fused gradient (data of 6 and 4
+    # doubles sorted into camera order by SortSlot0InputsAnyKernel)
+    assert info_f.num_fused_gradient_groups == (0 if name.startswith("Rigid") else 1), name
     assert fast[0] and gen[0]
     assert abs(fast[1] - gen[1]) <= 1e-13 * abs(gen[1]), (name, fast[1], gen[1])
     for k, what in ((2, "residuals"), (3, "gradient"), (4, "jacobian")):

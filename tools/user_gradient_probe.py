@@ -3,8 +3,10 @@
 the library kind of the same functor, on one problem-13682-shaped Program.
 
 The library's SnavelyKind takes the fused gradient (points in the
-evaluation, camera rows re-evaluated in camera order: gradient_mode 0); a
-user kind takes the gradient post-passes over the written Jacobian.  Times
+evaluation, camera rows re-evaluated in camera order: gradient_mode 0).  A
+user kind took the gradient post-passes over the written Jacobian until
+ABI 5 (profiles/round6/r6v: 4.21 ms against 1.97); since, it takes the same
+fused form through its own TU's launches (r6w).  Times
 both (device-resident, HIP-event-free wall time over --steps evaluations)
 with and without the gradient, and checks the gradients agree to 1e-13.
 
