@@ -364,6 +364,14 @@ bool FusedKind(int kind) {
   return kind == CSE_FUNCTOR_SNAVELY_2_9_3 || kind == kKindQuaternionTangent;
 }
 
+// The Jacobian operators built for the Snavely shape (CgnrMultiplyKernel,
+// the Schur kernels) read only the Jacobian's values, so they serve every
+// fused-gradient group of that shape -- 2 residuals, blocks of 9 (tangent)
+// and 3 -- the library's kinds and user kinds alike.
+bool SnavelyShaped(const Group& G) {
+  return G.shape.nb == 2 && G.shape.nr == 2 && G.shape.s0 == 9 && G.shape.s1 == 3;
+}
+
 // f(std::integral_constant<int, s0>) for the slot-0 sizes the fused
 // gradient's tail is built for (1..16, the affine kernels' bound).
 template <class F>
@@ -1221,7 +1229,7 @@ int BuildSchurPlan(cse_evaluator* ev, const cse_problem_desc* d, hipStream_t s) 
   S.eligible = false;
   if (ev->groups.size() != 1 || d->num_groups != 1) return CSE_OK;
   const Group& G = ev->groups[0];
-  if (!G.fuse_ok || G.policy != kAffinePacked || !FusedKind(G.kind) ||
+  if (!G.fuse_ok || G.policy != kAffinePacked || !SnavelyShaped(G) ||
       !ev->has_layout || ev->num_constant > 0)
     return CSE_OK;
   const cse_residual_group& g = d->groups[0];
@@ -1996,7 +2004,7 @@ int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const 
                        dim3((unsigned)((ev->num_effective + cse::kBlockThreads - 1) / cse::kBlockThreads)),
                        dim3(cse::kBlockThreads), 0, s, d_D, d_x, d_y, ev->num_effective);
   bool fused = true;
-  for (auto& G : ev->groups) fused = fused && (G.n == 0 || (G.fuse_ok && !G.const0 && FusedKind(G.kind)));
+  for (auto& G : ev->groups) fused = fused && (G.n == 0 || (G.fuse_ok && !G.const0 && SnavelyShaped(G)));
   if (!fused) {
     // z = J x, then y += J^T z: the two products of CudaCgnrLinearOperator.
     int rc;
@@ -2127,7 +2135,8 @@ int SchurCheck(cse_evaluator* ev, bool need_ready) {
   CSE_SINGLE_DEVICE(ev, "cse_schur");
   if (!ev->schur.eligible)
     return Fail(CSE_ERR_UNSUPPORTED,
-                "implicit Schur complement: needs one Snavely group on the affine BlockSparse path "
+                "implicit Schur complement: needs one Snavely-shaped group (2 residuals, blocks of 9 and 3) "
+                "on the affine BlockSparse path "
                 "with its points (slot 1) as the leading e columns and its cameras after them");
   if (need_ready && !ev->schur.ready) return Fail(CSE_ERR_INVALID, "cse_schur_init has not run");
   CSE_HIP(hipSetDevice(ev->device));

@@ -420,8 +420,10 @@ int cse_cgnr_multiply(cse_evaluator* ev, const double* d_jacobian_values, const 
  * (A^T A + D^2) [y_e; y_f] = A^T b is reduced to
  *     S y_f = rhs,  S = F^T F + D_f^2 - F^T E (E^T E + D_e^2)^-1 E^T F,
  *     rhs = F^T (b - E (E^T E + D_e^2)^-1 E^T b).
- * Requires (CSE_ERR_UNSUPPORTED otherwise) one Snavely group on the affine
- * BlockSparseMatrix path whose points occupy the effective columns
+ * Requires (CSE_ERR_UNSUPPORTED otherwise) one group of the Snavely shape
+ * (2 residuals, a camera of 9 tangent parameters, a point of 3: the
+ * library's Snavely kinds or a user kind; the operators read only the
+ * Jacobian) on the affine BlockSparseMatrix path whose points occupy the effective columns
  * [0, num_cols_e) and cameras the rest, as ITERATIVE_SCHUR's elimination
  * ordering gives.  All device pointers, asynchronous on the evaluator's
  * stream, deterministic. */

@@ -63,13 +63,26 @@ def close(a, b, tol=RTOL):
     return np.linalg.norm(a - b) <= tol * max(np.linalg.norm(b), 1e-300)
 
 
-@pytest.mark.parametrize("which", ["bal", "runs", "quaternion"])
+def user_kind_program(name="SnavelyReprojectionError/Huber"):
+    """The BAL problem with a user functor kind of the Snavely shape
+    (examples/user_functors.hip): the operators read only the Jacobian.
+    (BundlerResidual's 9 x 9 camera blocks of F^T F reach condition numbers
+    near 1e10 on this problem, beyond the preconditioner check's 1e-11.)"""
+    import dataclasses
+    import user_functors as U
+    prog = bal.synthetic_program((10, 300, 1500), loss=ca.Loss.huber(1.0), seed=9)
+    prog.groups = [dataclasses.replace(g, kind=U.kind(name)) for g in prog.groups]
+    return prog
+
+
+@pytest.mark.parametrize("which", ["bal", "runs", "quaternion", "user"])
 @pytest.mark.parametrize("precond", [_cse.SCHUR_IDENTITY, _cse.SCHUR_JACOBI,
                                      _cse.SCHUR_SCHUR_JACOBI])
 def test_schur_operators_match_dense(gpu, which, precond):
     # quaternion: cameras on ProductManifold<QuaternionManifold, EuclideanManifold<6>>
-    # (9 tangent columns per f block, as the angle-axis camera).
-    prog = (runs_problem() if which == "runs" else
+    # (9 tangent columns per f block, as the angle-axis camera).  user: the
+    # Snavely functor as a user kind (its own TU) on the same operators.
+    prog = (runs_problem() if which == "runs" else user_kind_program() if which == "user" else
             bal.synthetic_program((10, 300, 1500), loss=ca.Loss.huber(1.0), seed=9,
                                   quaternion_manifold=which == "quaternion"))
     dev = torch.device("cuda", 0)
@@ -165,6 +178,19 @@ def test_schur_refuses_other_structures(gpu):
     prog = bal.synthetic_program((10, 300, 1500), format=ca.COMPRESSED_ROW, seed=9)
     ev = ca.Evaluator(prog)
     with pytest.raises(RuntimeError, match="cse_schur_structure"):
+        ev.schur_structure()
+    ev.close()
+    # a user kind of another camera size (<2, 7, 3>): not the operators' shape
+    import dataclasses
+    import user_functors as U
+    cams, pts, ci, pi, obs = bal.synthetic(10, 300, 1500, seed=9)
+    p7 = bal.program(np.ascontiguousarray(cams[:, :7]), pts, ci, pi, obs,
+                     kind=_cse.SNAVELY_NO_DISTORTION_2_7_3)
+    p7.groups = [dataclasses.replace(g, kind=U.kind("SnavelyReprojectionErrorNoRadialDistortion/Trivial"))
+                 for g in p7.groups]
+    ev = ca.Evaluator(p7)
+    assert ev.info().num_fused_gradient_groups == 1  # the fused gradient, not the operators
+    with pytest.raises(RuntimeError, match="Snavely-shaped"):
         ev.schur_structure()
     ev.close()
 

@@ -230,6 +230,17 @@ def test_cgnr_operator_matches_dense(gpu, fmt, shape):
     assert fused == (0 if np.all(np.diff(cams) >= 0) else 1)
 
 
+@pytest.mark.parametrize("fmt", [ca.BLOCK_SPARSE, ca.COMPRESSED_ROW])
+def test_cgnr_operator_user_kind(gpu, fmt):
+    # A user functor kind of the Snavely shape (BundlerResidual, its own TU)
+    # takes the one-pass operator: it reads only the Jacobian.
+    import dataclasses
+    import user_functors as U
+    prog = bal.synthetic_program((24, 3000, 20000), loss=ca.Loss.huber(1.0), format=fmt, seed=4)
+    prog.groups = [dataclasses.replace(g, kind=U.kind("BundlerResidual/Huber")) for g in prog.groups]
+    assert cgnr_op_check(prog, seed=3) == 1
+
+
 def test_cgnr_operator_two_product_path(gpu):
     # The mini bundle-adjustment problem (manifolds, constant blocks, three
     # functor types): not eligible for the fused pass.
