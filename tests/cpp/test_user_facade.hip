@@ -240,7 +240,36 @@ static void BundlerWithUserLoss(JacobianFormat format) {
               crs ? "CRS" : "BSM", cost, ocost);
 }
 
+// cse_register_functor's checks on the fused gradient's launches (ABI 5):
+// the header fills them for <NR, S0, 3> shapes only, and a table with some
+// of them missing, or built against another CamGradArgs, is refused.
+static void FusedGradientRegistration() {
+  using KB = cse::UserKind<user::BundlerResidual, void, 2, 9, 3>;
+  using KR = cse::UserKind<user::RigidAlignmentError, void, 3, 6>;
+  const cse_functor_ops ob = autodiff_internal::MakeOps<KB, cse::kLossTrivial>("fused check");
+  const cse_functor_ops orr = autodiff_internal::MakeOps<KR, cse::kLossTrivial>("rigid check");
+  EXPECT(ob.fused_points[0] && ob.fused_points[1] && ob.camera_gradient &&
+         ob.camera_gradient_args_size > 0);
+  EXPECT(!orr.fused_points[0] && !orr.fused_points[1] && !orr.camera_gradient &&
+         orr.camera_gradient_args_size == 0);
+  int32_t kind = -1;
+  cse_functor_ops bad = ob;
+  bad.camera_gradient = nullptr;
+  EXPECT(cse_register_functor(&bad, &kind) == CSE_ERR_INVALID && kind == -1);
+  bad = ob;
+  bad.camera_gradient_args_size += 8;
+  EXPECT(cse_register_functor(&bad, &kind) == CSE_ERR_INVALID && kind == -1);
+  bad = orr;
+  bad.fused_points[0] = ob.fused_points[0];
+  bad.fused_points[1] = ob.fused_points[1];
+  bad.camera_gradient = ob.camera_gradient;
+  bad.camera_gradient_args_size = ob.camera_gradient_args_size;
+  EXPECT(cse_register_functor(&bad, &kind) == CSE_ERR_INVALID && kind == -1);
+  EXPECT(cse_register_functor(&ob, &kind) == CSE_OK && kind >= CSE_FUNCTOR_USER_FIRST);
+}
+
 int main() {
+  FusedGradientRegistration();
   MiniBundleAdjustment(JacobianFormat::kBlockSparse);
   MiniBundleAdjustment(JacobianFormat::kCompressedRow);
   BundlerWithUserLoss(JacobianFormat::kBlockSparse);
