@@ -280,6 +280,8 @@ struct Group {
   DevBuf<double> sdata;
   DevBuf<int32_t> sid1;
   bool sorted_ready = false;
+  // Table policy: each 64-block chunk's store runs (BuildTableRuns).
+  DevBuf<int64_t> runs;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -1054,7 +1056,94 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   std::memcpy(a.user_loss, G.loss.user, sizeof(a.user_loss));
   a.apply_loss = ev->opts.apply_loss_function;
   a.check_finite = ev->opts.check_finite;
+  a.table_runs = G.runs.p;
   return a;
+}
+
+// The general kernel's store runs, found once per 64-block chunk (the
+// wave's blocks) by the tests TableStores makes on the device: flags
+// kTableRunFlagResiduals when the chunk's residuals are one run (NR apart),
+// kTableRunFlagBsm / Crs when every slot is active in all or none of its
+// blocks with one tangent size and its Jacobian rows form BlockSparseMatrix
+// cell runs / CompressedRow row blocks; then the residual run's start and
+// each active slot's first row.  [chunks][2 + nb]; shapes the kernel stages
+// (kTableStaged: NR x N <= 32) only.
+int BuildTableRuns(const cse_evaluator* ev, const cse_problem_desc* d, const cse_residual_group& g, Group* G,
+                   hipStream_t s) {
+  const KindShape& k = G->shape;
+  int N = 0;
+  for (int j = 0; j < k.nb; ++j) N += k.sz[j];
+  if (G->affine || G->n == 0 || k.nr * N > 32) return CSE_OK;
+  const int NB = k.nb, NR = k.nr, W = 2 + NB;
+  const int64_t n = G->n, nch = (n + cse::kWave - 1) / cse::kWave;
+  std::vector<int64_t> runs((size_t)(nch * W), 0);
+  auto gidx = [&](int64_t i) { return g.residual_block_index ? g.residual_block_index[i] : g.first_residual_block + i; };
+  auto pb = [&](int64_t i, int j) -> const cse_parameter_block& {
+    return d->parameter_blocks[g.parameter_block_ids[i * NB + j]];
+  };
+  for (int64_t c = 0; c < nch; ++c) {
+    const int64_t i0 = c * cse::kWave;
+    const int nb = (int)std::min<int64_t>(cse::kWave, n - i0);
+    int64_t* R = &runs[(size_t)(c * W)];
+    const int64_t off0 = d->residual_layout[gidx(i0)];
+    bool rr = true;
+    for (int l = 1; rr && l < nb; ++l) rr = d->residual_layout[gidx(i0 + l)] == off0 + (int64_t)NR * l;
+    if (rr) {
+      R[0] |= cse::kTableRunFlagResiduals;
+      R[1] = off0;
+    }
+    if (!ev->has_layout) continue;
+    bool cst[CSE_MAX_PARAMETER_BLOCKS];
+    int t[CSE_MAX_PARAMETER_BLOCKS];
+    bool uniform = true;
+    for (int j = 0; j < NB; ++j) {
+      cst[j] = pb(i0, j).is_constant != 0;
+      t[j] = pb(i0, j).tangent_size;
+      for (int l = 1; uniform && l < nb; ++l) {
+        const cse_parameter_block& p = pb(i0 + l, j);
+        uniform = (p.is_constant != 0) == cst[j] && (cst[j] || p.tangent_size == t[j]);
+      }
+    }
+    if (!uniform) continue;
+    // Row (j, kk) of lane l: offsets[layout[gidx] + a NR + kk], a = slot j's
+    // position among the active slots.
+    auto row = [&](int l, int a, int kk) {
+      return d->jacobian_per_residual_offsets[d->jacobian_per_residual_layout[gidx(i0 + l)] + (int64_t)a * NR + kk];
+    };
+    int64_t base[CSE_MAX_PARAMETER_BLOCKS] = {0};
+    int64_t r0 = INT64_MAX;
+    int w = 0, a = 0;
+    for (int j = 0; j < NB; ++j) {
+      if (cst[j]) continue;
+      base[j] = row(0, a++, 0);
+      r0 = std::min(r0, base[j]);
+      w += t[j];
+    }
+    bool bsm = true, crs = true;
+    a = 0;
+    for (int j = 0; j < NB; ++j) {
+      if (cst[j]) continue;
+      for (int l = 0; l < nb && (bsm || crs); ++l)
+        for (int kk = 0; kk < NR; ++kk) {
+          const int64_t v = row(l, a, kk);
+          bsm = bsm && v == base[j] + (int64_t)l * NR * t[j] + (int64_t)kk * t[j];
+          crs = crs && v == base[j] + (int64_t)l * NR * w + (int64_t)kk * w;
+        }
+      ++a;
+      const int64_t cj = base[j] - r0;
+      crs = crs && cj >= 0 && cj + t[j] <= w;
+      for (int j2 = 0; j2 < j; ++j2) {
+        if (cst[j2]) continue;
+        const int64_t c2 = base[j2] - r0;
+        crs = crs && (cj + t[j] <= c2 || c2 + t[j2] <= cj);
+      }
+    }
+    R[0] |= (bsm ? cse::kTableRunFlagBsm : 0) | (crs ? cse::kTableRunFlagCrs : 0);
+    for (int j = 0; j < NB; ++j) R[2 + j] = base[j];
+  }
+  int rc = G->runs.upload(runs.data(), runs.size(), s);
+  if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = Fail(CSE_ERR_HIP, "table runs upload failed");
+  return rc;
 }
 
 int FoldTiming(cse_evaluator* ev) {
@@ -1757,6 +1846,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
                                     : 1)))
           return bail(rc);
     }
+    if ((rc = BuildTableRuns(ev, d, g, &G, s))) return bail(rc);
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
     if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
     if ((!G.affine || G.const0) && g.residual_block_index &&

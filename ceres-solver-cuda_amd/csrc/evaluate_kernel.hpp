@@ -1473,9 +1473,13 @@ __global__ __launch_bounds__(kBlockThreads) void SortSlot0InputsAnyKernel(const 
 // layouts) each lane scatters its rows through the offset tables as
 // WriteJacobians does (cuda_evaluator_kernel.h:260-294).  A failed block's
 // outputs are unspecified (the evaluation reports the failure), so the
-// staged runs carry them along.
+// staged runs carry them along.  With a.table_runs (BuildTableRuns: the
+// same tests, made once per chunk at cse_create) the wave takes its run
+// starts from there and loads no per-block offsets (at two slots and two
+// residuals 48 of the kernel's table bytes a block, profiles/round6/r6gen).
 template <class K>
 constexpr bool kTableStaged = KindTraits<K>::NR * KindTraits<K>::N <= 32;
+constexpr int kTableRunFlagResiduals = 1, kTableRunFlagBsm = 2, kTableRunFlagCrs = 4;
 
 template <class K, bool kJac>
 __device__ __forceinline__ void TableStores(const GroupArgs& a, bool active, bool ok, int64_t gi,
@@ -1494,10 +1498,20 @@ __device__ __forceinline__ void TableStores(const GroupArgs& a, bool active, boo
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   };
+  // This wave's chunk record (wave-uniform: scalar loads).
+  const int64_t* run = nullptr;
+  int64_t flags = 0;
+  if constexpr (kStaged) {
+    if (a.table_runs) {
+      const int64_t c = (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+      run = a.table_runs + c * (2 + NB);
+      flags = run[0];
+    }
+  }
   if (a.residuals) {
-    const int64_t off = active ? a.residual_layout[gi] : 0;
-    const int64_t off0 = __shfl(off, 0, kWave);
-    if (kStaged && all(off == off0 + (int64_t)NR * lane)) {
+    const int64_t off = active && !(flags & kTableRunFlagResiduals) ? a.residual_layout[gi] : 0;
+    const int64_t off0 = run ? run[1] : __shfl(off, 0, kWave);
+    if (kStaged && (run ? (flags & kTableRunFlagResiduals) != 0 : all(off == off0 + (int64_t)NR * lane))) {
       if (active) {
 #pragma unroll
         for (int k = 0; k < NR; ++k) st[lane * NR + k] = r[k];
@@ -1514,7 +1528,7 @@ __device__ __forceinline__ void TableStores(const GroupArgs& a, bool active, boo
     if (!a.jacobian) return;
     // Row (j, k) of slot j's a-th active position goes to
     // values + offsets[layout[gi] + a NR + k].
-    const int64_t q = active ? a.jac_layout[gi] : 0;
+    const int64_t q = active && !run ? a.jac_layout[gi] : 0;
     bool uniform = kStaged;
     bool cst[NB];
     int t[NB];
@@ -1530,21 +1544,22 @@ __device__ __forceinline__ void TableStores(const GroupArgs& a, bool active, boo
       uniform = uniform && all(pb[j].is_constant || pb[j].tangent_size == t[j]);
 #pragma unroll
       for (int k = 0; k < NR; ++k)
-        row[j][k] = active && !cst[j] ? a.jac_offsets[q + (int64_t)na * NR + k] : 0;
+        row[j][k] = active && !cst[j] && !run ? a.jac_offsets[q + (int64_t)na * NR + k] : 0;
       if (!cst[j]) ++na;
     }
-    bool bsm = uniform, crs = uniform;
+    bool bsm = run ? (flags & kTableRunFlagBsm) != 0 : uniform;
+    bool crs = run ? (flags & kTableRunFlagCrs) != 0 : uniform;
     int64_t base[NB];
     int64_t r0 = INT64_MAX;
     int w = 0;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      base[j] = __shfl(row[j][0], 0, kWave);
+      base[j] = run ? run[2 + j] : __shfl(row[j][0], 0, kWave);
       if (cst[j]) continue;
       r0 = base[j] < r0 ? base[j] : r0;
       w += t[j];
     }
-    if (uniform) {
+    if (uniform && !run) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if (cst[j]) continue;
@@ -1601,7 +1616,7 @@ __device__ __forceinline__ void TableStores(const GroupArgs& a, bool active, boo
       for (int p = lane; p < nb * blk; p += kWave) a.jacobian[r0 + p] = st[p];
       sync();
     } else if (active && ok) {
-      int64_t qq = q;
+      int64_t qq = run ? a.jac_layout[gi] : q;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if (pb[j].is_constant) continue;

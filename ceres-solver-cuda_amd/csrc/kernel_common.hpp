@@ -90,12 +90,16 @@ struct GroupArgs {
   int check_finite;
   // kLossUser: the bytes of the group's loss object (cse_loss.user).
   double user_loss[kUserLossDoubles];
+  // Table policy, found at cse_create (BuildTableRuns): per 64-block chunk
+  // [flags, residual run start, first cell / row segment of each slot];
+  // null = the kernel finds the runs from the offset tables.
+  const int64_t* table_runs;
 };
 
 // Layout tag of the argument blocks (GroupArgs, GradArgs, CamGradArgs),
 // checked when a user functor kind registers kernels compiled in another TU
 // (cse_register_functor): bump on any change to them.
-constexpr uint64_t kGroupArgsTag = 0x6373654761310003ull;
+constexpr uint64_t kGroupArgsTag = 0x6373654761310004ull;
 
 // Compile-time shape of a functor kind: kR residuals, NB parameter blocks
 // of sizes kSizes[0..NB) concatenated into N columns.
