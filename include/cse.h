@@ -215,7 +215,8 @@ typedef struct cse_options {
                                    slot-0 contributions written in block order and
                                    summed per block (the round-2 form), else 1.
                                    0, 1 and 3 are bit-deterministic.  With
-                                   jacobian_form CSE_JACOBIAN_JET, 3 runs as 1. */
+                                   jacobian_form CSE_JACOBIAN_JET, and for user
+                                   kinds, 3 runs as 1. */
   int32_t jacobian_form;        /* cse_jacobian_form: how the SnavelyReprojectionError
                                    Jacobian is differentiated (every other kind always
                                    uses Jet<double, N>, AutoDifferentiate) */
