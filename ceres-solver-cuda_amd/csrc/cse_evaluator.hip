@@ -280,8 +280,11 @@ struct Group {
   DevBuf<double> sdata;
   DevBuf<int32_t> sid1;
   bool sorted_ready = false;
-  // Table policy: each 64-block chunk's store runs (BuildTableRuns).
+  // Table policy: each 64-block chunk's store runs (BuildTableRuns), and
+  // slot 0 plain in every block (DetectPlain0).
   DevBuf<int64_t> runs;
+  bool plain0 = false;
+  int64_t plain0_state_base = 0, plain0_delta_base = 0;
 };
 
 using LaunchFn = void (*)(const cse::GroupArgs&, int64_t num_wg, hipStream_t);
@@ -1057,7 +1060,37 @@ cse::GroupArgs MakeArgs(cse_evaluator* ev, Group& G, const double* state, double
   a.apply_loss = ev->opts.apply_loss_function;
   a.check_finite = ev->opts.check_finite;
   a.table_runs = G.runs.p;
+  a.plain0 = G.plain0 ? 1 : 0;
+  a.plain0_state_base = G.plain0_state_base;
+  a.plain0_delta_base = G.plain0_delta_base;
   return a;
+}
+
+// A table group whose slot-0 blocks are all plain: active, no manifold
+// (plus_jacobian_offset -1), tangent size = size = the kind's, state and
+// delta offsets affine in the id.  EvaluateTableKernel then forms their PbDev
+// records instead of loading them: one cache line less per lane for a
+// camera-like slot 0, whose lines the point stream evicts from L2 between
+// uses.
+void DetectPlain0(const cse_problem_desc* d, const cse_residual_group& g, Group* G) {
+  const KindShape& k = G->shape;
+  G->plain0 = false;
+  if (G->affine || G->n == 0) return;
+  const int S = k.sz[0];
+  const int32_t id0 = g.parameter_block_ids[0];
+  const int64_t sb = d->parameter_blocks[id0].state_offset - (int64_t)S * id0;
+  const int64_t db = d->parameter_blocks[id0].delta_offset - (int64_t)S * id0;
+  for (int64_t i = 0; i < G->n; ++i) {
+    const int32_t id = g.parameter_block_ids[i * k.nb];
+    const cse_parameter_block& p = d->parameter_blocks[id];
+    if (p.is_constant || p.manifold != CSE_MANIFOLD_MATRIX || p.plus_jacobian_offset != -1 ||
+        p.size != S || p.tangent_size != S || p.state_offset != sb + (int64_t)S * id ||
+        p.delta_offset != db + (int64_t)S * id)
+      return;
+  }
+  G->plain0 = true;
+  G->plain0_state_base = sb;
+  G->plain0_delta_base = db;
 }
 
 // The general kernel's store runs, found once per 64-block chunk (the
@@ -1847,6 +1880,7 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
           return bail(rc);
     }
     if ((rc = BuildTableRuns(ev, d, g, &G, s))) return bail(rc);
+    DetectPlain0(d, g, &G);
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
     if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
     if ((!G.affine || G.const0) && g.residual_block_index &&

@@ -1670,7 +1670,13 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const Group
     double x[N];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      pb[j] = a.pbs[a.ids[i * NB + j]];
+      const int32_t id = a.ids[i * NB + j];
+      if (j == 0 && a.plain0) {  // the record the table holds, without its cache line
+        constexpr int S = Tr::Size(0);
+        pb[0] = PbDev{a.plain0_state_base + (int64_t)S * id, a.plain0_delta_base + (int64_t)S * id, -1, S, 0};
+      } else {
+        pb[j] = a.pbs[id];
+      }
       const double* p = (pb[j].is_constant ? a.cstate : a.state) + pb[j].state_offset;
 #pragma unroll
       for (int c = 0; c < Tr::Size(j); ++c) x[Tr::Off(j) + c] = p[c];

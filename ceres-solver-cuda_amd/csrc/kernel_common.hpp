@@ -94,12 +94,17 @@ struct GroupArgs {
   // [flags, residual run start, first cell / row segment of each slot];
   // null = the kernel finds the runs from the offset tables.
   const int64_t* table_runs;
+  // Table policy, slot 0 plain in every block (active, no manifold, tangent
+  // size = size, state and delta offsets affine in the id; DetectPlain0):
+  // its PbDev is formed from these, not loaded.
+  int64_t plain0_state_base, plain0_delta_base;
+  int32_t plain0;
 };
 
 // Layout tag of the argument blocks (GroupArgs, GradArgs, CamGradArgs),
 // checked when a user functor kind registers kernels compiled in another TU
 // (cse_register_functor): bump on any change to them.
-constexpr uint64_t kGroupArgsTag = 0x6373654761310004ull;
+constexpr uint64_t kGroupArgsTag = 0x6373654761310005ull;
 
 // Compile-time shape of a functor kind: kR residuals, NB parameter blocks
 // of sizes kSizes[0..NB) concatenated into N columns.
