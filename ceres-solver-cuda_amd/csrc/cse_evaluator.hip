@@ -1881,6 +1881,25 @@ int cse_create(const cse_problem_desc* d, const cse_options* options, cse_evalua
     }
     if ((rc = BuildTableRuns(ev, d, g, &G, s))) return bail(rc);
     DetectPlain0(d, g, &G);
+    if (G.plain0) {
+      // A plain slot 0 of a small id range (the cameras) is read from a
+      // repacked copy, as the affine kernels read it (RepackSlot0Kernel, every
+      // evaluation): one 128-byte row a lane instead of its values at an
+      // 8-byte alignment.
+      int32_t lo = INT32_MAX, hi = INT32_MIN;
+      for (int64_t i = 0; i < g.num_blocks; ++i) {
+        lo = std::min(lo, g.parameter_block_ids[i * k.nb]);
+        hi = std::max(hi, g.parameter_block_ids[i * k.nb]);
+      }
+      const int64_t count = (int64_t)hi - lo + 1;
+      if (k.sz[0] <= 16 && count <= (1 << 20)) {
+        G.slot0_lo = lo;
+        G.slot0_count = count;
+        G.packed_stride = cse::PackedRowDoubles(k.sz[0]);
+        G.state_base[0] = G.plain0_state_base;
+        if ((rc = G.packed0.alloc((size_t)count * G.packed_stride))) return bail(rc);
+      }
+    }
     if ((rc = G.ids.upload(g.parameter_block_ids, (size_t)g.num_blocks * k.nb, s))) return bail(rc);
     if ((rc = G.data.upload(g.functor_data, (size_t)g.num_blocks * k.data, s))) return bail(rc);
     if ((!G.affine || G.const0) && g.residual_block_index &&

@@ -1671,13 +1671,19 @@ __global__ __launch_bounds__(kBlockThreads) void EvaluateTableKernel(const Group
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int32_t id = a.ids[i * NB + j];
+      const double* p;
       if (j == 0 && a.plain0) {  // the record the table holds, without its cache line
         constexpr int S = Tr::Size(0);
         pb[0] = PbDev{a.plain0_state_base + (int64_t)S * id, a.plain0_delta_base + (int64_t)S * id, -1, S, 0};
+        // the values from the repacked copy when there is one (one aligned
+        // 128-byte row), else from the state
+        p = a.packed0 ? static_cast<const double*>(__builtin_assume_aligned(
+                            a.packed0 + (int64_t)a.packed0_stride * (id - a.packed0_lo), 16))
+                      : a.state + pb[0].state_offset;
       } else {
         pb[j] = a.pbs[id];
+        p = (pb[j].is_constant ? a.cstate : a.state) + pb[j].state_offset;
       }
-      const double* p = (pb[j].is_constant ? a.cstate : a.state) + pb[j].state_offset;
 #pragma unroll
       for (int c = 0; c < Tr::Size(j); ++c) x[Tr::Off(j) + c] = p[c];
     }
